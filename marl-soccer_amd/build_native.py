@@ -1,0 +1,60 @@
+"""Build the HIP library in-tree: marl-soccer_amd/lib/libmarlsoccer.so (gfx950 only).
+
+    python marl-soccer_amd/build_native.py [--force] [--verbose]
+
+hipcc cross-compiles without a GPU. The build is skipped when the .so is newer than
+every source.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIB_DIR, "libmarlsoccer.so")
+SOURCES = [os.path.join(CSRC, "ms_env.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, "ms_device.h"), os.path.join(ROOT, "include", "marl_soccer.h")]
+ARCH = os.environ.get("MS_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", f"--offload-arch={ARCH}"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the MI355X library cannot be built")
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(d) <= t for d in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB
+    os.makedirs(LIB_DIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), *FLAGS, "-o", tmp, *SOURCES]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    a = ap.parse_args()
+    print(build(a.force, a.verbose))
+    sys.exit(0)

@@ -1,0 +1,1066 @@
+// ms_env.hip — MI355X-native batched 2v2 soccer env: HIP kernels + the C-ABI of
+// include/marl_soccer.h.
+//
+// One fused kernel advances every environment by one env.step (SoccerEnv.step ->
+// Game.step -> pymunk Space.step(1/60); soccer_env.py:100-154, game/game.py:378-437).
+// One lane owns one env for the whole step: the physics of one env is a short sequential
+// Gauss-Seidel solve over at most a few contacts, so parallelism comes from the batch.
+//
+// HBM layout (struct-of-arrays, every plane is N contiguous elements so a wavefront's
+// 64 lanes touch 64 consecutive words):
+//   F  float [PL_F][N]   bodies (44 planes) + 3-frame history ring (2 x 4 x 22 planes)
+//   I  int32 [PL_I][N]   steps, score, meta bits, PCG64 buffered u32
+//   R  u64   [4][N]      PCG64 state/increment (touched only by resets and goal respawns)
+//   CH u32   [2][MAXA][N] arbiter-cache headers, ping-pong by a per-env parity bit
+//   CJ float [2][MAXA][4][N] arbiter-cache accumulated impulses (jn0, jt0, jn1, jt1)
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <random>
+#include <string>
+
+#include "ms_device.h"
+
+using namespace ms;
+
+#define MS_BLOCK 64
+#define MAXA MS_MAX_ARBITERS
+
+// ---- plane indices -----------------------------------------------------------------------
+enum {
+  // agent b (0..3): base b*9: PX PY VX VY ANG W VBX VBY WB ; ball: base 36: PX PY VX VY W VBX VBY WB
+  F_BALL = 36,
+  F_HIST = 44,            // [slot 2][agent 4][22]
+  PL_F = 44 + 2 * 4 * 22  // 220
+};
+enum { I_STEPS = 0, I_SCORE = 1, I_META = 2, I_U32 = 3, PL_I = 4 };
+// META bits: 0-1 spawn mode, 2 hist_empty, 3 ring head (slot holding t-1), 4 cache parity,
+//            8-13 n_cache, 16 PCG64 has_uint32
+#define META_MODE(m) ((m) & 3)
+#define META_HE 4u
+#define META_RING 8u
+#define META_PAR 16u
+#define META_NC(m) (((m) >> 8) & 63)
+#define META_H32 (1u << 16)
+
+struct DevState {
+  float* F;
+  int32_t* I;
+  uint64_t* R;
+  uint32_t* CH;
+  float* CJ;
+  int64_t n;
+};
+
+struct Counters {
+  unsigned long long overflow;
+  unsigned long long nonfinite;
+  long long first_bad;
+};
+
+__device__ __forceinline__ float& AGF(const DevState& S, int b, int f, int64_t e) { return S.F[(int64_t)(b * 9 + f) * S.n + e]; }
+
+// ---- per-lane env register file ------------------------------------------------------------
+struct Env {
+  float px[5], py[5], vx[5], vy[5], ang[4], w[5], vbx[5], vby[5], wb[5];
+  int steps, score_blue, score_red;
+  uint32_t meta;
+  Rng rng;
+};
+
+__device__ __forceinline__ void load_bodies(const DevState& S, int64_t e, Env& E) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    E.px[b] = AGF(S, b, 0, e); E.py[b] = AGF(S, b, 1, e);
+    E.vx[b] = AGF(S, b, 2, e); E.vy[b] = AGF(S, b, 3, e);
+    E.ang[b] = AGF(S, b, 4, e); E.w[b] = AGF(S, b, 5, e);
+    E.vbx[b] = AGF(S, b, 6, e); E.vby[b] = AGF(S, b, 7, e); E.wb[b] = AGF(S, b, 8, e);
+  }
+  const int64_t n = S.n;
+  E.px[4] = S.F[(F_BALL + 0) * n + e]; E.py[4] = S.F[(F_BALL + 1) * n + e];
+  E.vx[4] = S.F[(F_BALL + 2) * n + e]; E.vy[4] = S.F[(F_BALL + 3) * n + e];
+  E.w[4] = S.F[(F_BALL + 4) * n + e];
+  E.vbx[4] = S.F[(F_BALL + 5) * n + e]; E.vby[4] = S.F[(F_BALL + 6) * n + e];
+  E.wb[4] = S.F[(F_BALL + 7) * n + e];
+}
+
+__device__ __forceinline__ void store_bodies(const DevState& S, int64_t e, const Env& E) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    AGF(S, b, 0, e) = E.px[b]; AGF(S, b, 1, e) = E.py[b];
+    AGF(S, b, 2, e) = E.vx[b]; AGF(S, b, 3, e) = E.vy[b];
+    AGF(S, b, 4, e) = E.ang[b]; AGF(S, b, 5, e) = E.w[b];
+    AGF(S, b, 6, e) = E.vbx[b]; AGF(S, b, 7, e) = E.vby[b]; AGF(S, b, 8, e) = E.wb[b];
+  }
+  const int64_t n = S.n;
+  S.F[(F_BALL + 0) * n + e] = E.px[4]; S.F[(F_BALL + 1) * n + e] = E.py[4];
+  S.F[(F_BALL + 2) * n + e] = E.vx[4]; S.F[(F_BALL + 3) * n + e] = E.vy[4];
+  S.F[(F_BALL + 4) * n + e] = E.w[4];
+  S.F[(F_BALL + 5) * n + e] = E.vbx[4]; S.F[(F_BALL + 6) * n + e] = E.vby[4];
+  S.F[(F_BALL + 7) * n + e] = E.wb[4];
+}
+
+__device__ __forceinline__ void load_rng(const DevState& S, int64_t e, Env& E) {
+  const int64_t n = S.n;
+  E.rng.shi = S.R[0 * n + e]; E.rng.slo = S.R[1 * n + e];
+  E.rng.ihi = S.R[2 * n + e]; E.rng.ilo = S.R[3 * n + e];
+  E.rng.has32 = (E.meta & META_H32) ? 1u : 0u;
+  E.rng.u32 = (uint32_t)S.I[I_U32 * n + e];
+}
+__device__ __forceinline__ void store_rng(const DevState& S, int64_t e, Env& E) {
+  const int64_t n = S.n;
+  S.R[0 * n + e] = E.rng.shi; S.R[1 * n + e] = E.rng.slo;
+  S.R[2 * n + e] = E.rng.ihi; S.R[3 * n + e] = E.rng.ilo;
+  S.I[I_U32 * n + e] = (int32_t)E.rng.u32;
+  E.meta = (E.meta & ~META_H32) | (E.rng.has32 ? META_H32 : 0u);
+}
+
+// ---- frames -----------------------------------------------------------------------------
+__device__ __forceinline__ void frame_of(const Params& P, const Env& E, int agent, float* o) {
+  switch (agent) {
+    case 0: agent_frame<0>(P, E.px, E.py, E.vx, E.vy, E.ang, E.w, o); break;
+    case 1: agent_frame<1>(P, E.px, E.py, E.vx, E.vy, E.ang, E.w, o); break;
+    case 2: agent_frame<2>(P, E.px, E.py, E.vx, E.vy, E.ang, E.w, o); break;
+    default: agent_frame<3>(P, E.px, E.py, E.vx, E.vy, E.ang, E.w, o); break;
+  }
+}
+
+// Write the stacked obs for one env: [t-2, t-1, t] per agent (soccer_env.py:130-140) and
+// advance the history ring. reset: all three slots are the new frame (soccer_env.py:90-96).
+__device__ __forceinline__ void emit_frames(const DevState& S, const Params& P, int64_t e, Env& E, bool fill3,
+                                            float* __restrict__ obs) {
+  const int64_t n = S.n;
+  const int head = (E.meta & META_RING) ? 1 : 0;  // slot holding t-1; the other holds t-2
+  const int old = head ^ 1;
+#pragma unroll 1
+  for (int a = 0; a < 4; ++a) {
+    float f[22];
+    frame_of(P, E, a, f);
+    float* o = obs ? obs + e * 264 + a * 66 : nullptr;
+    if (fill3) {
+#pragma unroll
+      for (int k = 0; k < 22; ++k) {
+        S.F[(int64_t)(F_HIST + 0 * 88 + a * 22 + k) * n + e] = f[k];
+        S.F[(int64_t)(F_HIST + 1 * 88 + a * 22 + k) * n + e] = f[k];
+      }
+      if (o) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+          for (int k = 0; k < 22; k += 2) *(float2*)(o + s * 22 + k) = make_float2(f[k], f[k + 1]);
+      }
+    } else {
+      float* ho = S.F + (int64_t)(F_HIST + old * 88 + a * 22) * n + e;
+      float* hn = S.F + (int64_t)(F_HIST + head * 88 + a * 22) * n + e;
+      if (o) {
+#pragma unroll
+        for (int k = 0; k < 22; k += 2) {
+          *(float2*)(o + k) = make_float2(ho[k * n], ho[(k + 1) * n]);
+          *(float2*)(o + 22 + k) = make_float2(hn[k * n], hn[(k + 1) * n]);
+          *(float2*)(o + 44 + k) = make_float2(f[k], f[k + 1]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 22; ++k) ho[k * n] = f[k];  // new frame replaces t-2
+    }
+  }
+  if (fill3) E.meta &= ~(META_HE | META_RING);
+  else E.meta ^= META_RING;
+}
+
+// Game.reset (game.py:76-118): fresh bodies, score/steps 0, arbiters dropped, spawn.
+__device__ __forceinline__ void reset_env_regs(Env& E, int mode) {
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    E.vx[b] = 0.0f; E.vy[b] = 0.0f; E.w[b] = 0.0f;
+    E.vbx[b] = 0.0f; E.vby[b] = 0.0f; E.wb[b] = 0.0f;
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) E.ang[b] = b < 2 ? 0.0f : 3.14159265358979323846f;
+  E.steps = 0; E.score_blue = 0; E.score_red = 0;
+  E.meta = (E.meta & (META_H32 | META_PAR)) | (uint32_t)(mode & 3);  // n_cache = 0
+  spawn_positions(E.rng, mode, E.px, E.py);
+}
+
+// Goal soft reset (Game._reset_positions, game.py:120-127): bias velocities, ball spin and
+// the arbiter cache survive.
+__device__ __forceinline__ void soft_reset_regs(Env& E) {
+  spawn_positions(E.rng, META_MODE(E.meta), E.px, E.py);
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    E.vx[b] = 0.0f; E.vy[b] = 0.0f; E.w[b] = 0.0f;
+    E.ang[b] = b < 2 ? 0.0f : 3.14159265358979323846f;
+  }
+  E.vx[4] = 0.0f; E.vy[4] = 0.0f;
+}
+
+// ---- physics: cpSpaceStep restated ---------------------------------------------------------
+struct Contact {
+  float r1x, r1y, r2x, r2y, nMass, tMass, bias, bounce, jn, jt, jb;
+  int hash;
+};
+struct Arb {
+  int pair, ba, bb, count, warm;
+  float nx, ny, e, u;
+  Contact c[2];
+};
+
+// LDS body velocity file used by the solver: [field][body 0..5][lane]; body 5 = static (0).
+enum { SV_VX = 0, SV_VY, SV_W, SV_VBX, SV_VBY, SV_WB, SV_PX, SV_PY, SV_N };
+
+struct Lds {
+  float v[SV_N][6][MS_BLOCK];
+};
+
+__device__ __forceinline__ float cache_field(const DevState& S, int par, int k, int f, int64_t e) {
+  return S.CJ[((int64_t)(par * MAXA + k) * 4 + f) * S.n + e];
+}
+
+__device__ __forceinline__ void physics_step(const DevState& S, const Params& P, int64_t e, Env& E, float fx[4],
+                                             float fy[4], float tq[4], Lds& L, int lane,
+                                             unsigned long long* overflow_acc) {
+  const float dt = P.dt;
+  // cpBodyUpdatePosition
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    E.px[b] = E.px[b] + (E.vx[b] + E.vbx[b]) * dt;
+    E.py[b] = E.py[b] + (E.vy[b] + E.vby[b]) * dt;
+    if (b < 4) E.ang[b] = E.ang[b] + (E.w[b] + E.wb[b]) * dt;
+    E.vbx[b] = 0.0f; E.vby[b] = 0.0f; E.wb[b] = 0.0f;
+  }
+  Box box[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    float s, c;
+    sincos_contract(E.ang[b], &s, &c);
+    box_world(E.px[b], E.py[b], c, s, box[b]);
+  }
+  const V2 ballc = v2(E.px[4], E.py[4]);
+  const float BR = 10.0f;
+  const float ballbb[4] = {ballc.x - BR, ballc.y - BR, ballc.x + BR, ballc.y + BR};
+
+  const int par = (E.meta & META_PAR) ? 1 : 0;
+  const int nc = META_NC(E.meta);
+  Arb arb[MAXA];
+  int na = 0;
+  int cur = 0;  // merge cursor into the (pair-sorted) old cache
+  uint32_t curh = nc > 0 ? S.CH[(int64_t)(par * MAXA + 0) * S.n + e] : 0xffffffffu;
+
+  // narrowphase per shape pair in canonical order (cpSpaceCollideShapes + cpArbiterUpdate)
+  auto add_arbiter = [&](int p, int ba, int bb, const Col& col, float ee, float uu) {
+    if (na >= MAXA) { (*overflow_acc)++; return; }
+    while (cur < nc && (int)(curh & 63u) < p) {
+      ++cur;
+      curh = cur < nc ? S.CH[(int64_t)(par * MAXA + cur) * S.n + e] : 0xffffffffu;
+    }
+    const bool found = cur < nc && (int)(curh & 63u) == p;
+    Arb& A = arb[na++];
+    A.pair = p; A.ba = ba; A.bb = bb; A.count = col.count;
+    A.warm = found && ((curh >> 8) & 3u) == 0u;
+    A.nx = col.n.x; A.ny = col.n.y; A.e = ee; A.u = uu;
+    for (int k = 0; k < col.count; ++k) {
+      Contact& C = A.c[k];
+      float ax = 0.0f, ay = 0.0f, bx = 0.0f, by = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        if (q == ba) { ax = E.px[q]; ay = E.py[q]; }
+        if (q == bb) { bx = E.px[q]; by = E.py[q]; }
+      }
+      C.r1x = col.p1[k].x - ax; C.r1y = col.p1[k].y - ay;
+      C.r2x = col.p2[k].x - bx; C.r2y = col.p2[k].y - by;
+      C.hash = col.hash[k];
+      C.jn = 0.0f; C.jt = 0.0f;
+      if (found) {
+        const int ocount = (curh >> 6) & 3u;
+        for (int j = 0; j < ocount; ++j) {
+          const int oh = (curh >> (16 + 8 * j)) & 0xffu;
+          if (oh == C.hash) {
+            C.jn = cache_field(S, par, cur, 2 * j, e);
+            C.jt = cache_field(S, par, cur, 2 * j + 1, e);
+          }
+        }
+      }
+    }
+  };
+
+  // agent-agent (pairs 0-5)
+#pragma unroll
+  for (int p = 0; p < 6; ++p) {
+    const int i = p < 3 ? 0 : (p < 5 ? 1 : 2);
+    const int j = p == 0 ? 1 : (p == 1 ? 2 : (p == 2 ? 3 : (p == 3 ? 2 : 3)));
+    if (!bb_intersects(box[i].bb, box[j].bb)) continue;
+    Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
+    col_box_box(box[i], box[j], col);
+    if (col.count) add_arbiter(p, i, j, col, P.e_aa, P.u_aa);
+  }
+  // ball-agent (6-9)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (!bb_intersects(ballbb, box[i].bb)) continue;
+    Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
+    col_circle_box(ballc, BR, box[i], col);
+    if (col.count) add_arbiter(6 + i, 4, i, col, P.e_ab, P.u_ab);
+  }
+  // static-agent (10-41)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll 1
+    for (int s = 0; s < 8; ++s) {
+      if (!bb_intersects(P.seg[s].bb, box[i].bb)) continue;
+      Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
+      col_seg_box(P.seg[s], box[i], col);
+      if (col.count) add_arbiter(10 + i * 8 + s, 5, i, col, s < 6 ? P.e_aw : P.e_ag, s < 6 ? P.u_aw : P.u_ag);
+    }
+  }
+  // ball-wall (42-47)
+#pragma unroll 1
+  for (int s = 0; s < 6; ++s) {
+    if (!bb_intersects(ballbb, P.seg[s].bb)) continue;
+    Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
+    col_circle_seg(ballc, BR, P.seg[s], col);
+    if (col.count) add_arbiter(42 + s, 4, 5, col, P.e_bw, P.u_bw);
+  }
+
+  // stage positions + velocities in LDS for dynamic body indexing
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    L.v[SV_VX][b][lane] = E.vx[b]; L.v[SV_VY][b][lane] = E.vy[b]; L.v[SV_W][b][lane] = E.w[b];
+    L.v[SV_VBX][b][lane] = 0.0f; L.v[SV_VBY][b][lane] = 0.0f; L.v[SV_WB][b][lane] = 0.0f;
+    L.v[SV_PX][b][lane] = E.px[b]; L.v[SV_PY][b][lane] = E.py[b];
+  }
+#pragma unroll
+  for (int f = 0; f < SV_N; ++f) L.v[f][5][lane] = 0.0f;
+
+  // cpArbiterPreStep (pre-integration velocities)
+  for (int k = 0; k < na; ++k) {
+    Arb& A = arb[k];
+    const int ba = A.ba, bb = A.bb;
+    const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
+    const V2 n = v2(A.nx, A.ny);
+    const V2 body_delta = v2(L.v[SV_PX][bb][lane] - L.v[SV_PX][ba][lane], L.v[SV_PY][bb][lane] - L.v[SV_PY][ba][lane]);
+    const V2 va = v2(L.v[SV_VX][ba][lane], L.v[SV_VY][ba][lane]), vb = v2(L.v[SV_VX][bb][lane], L.v[SV_VY][bb][lane]);
+    const float wa = L.v[SV_W][ba][lane], wbv = L.v[SV_W][bb][lane];
+    for (int i = 0; i < A.count; ++i) {
+      Contact& C = A.c[i];
+      const V2 r1 = v2(C.r1x, C.r1y), r2 = v2(C.r2x, C.r2y);
+      float rcn1 = vcross(r1, n), rcn2 = vcross(r2, n);
+      C.nMass = 1.0f / ((ma + ia * rcn1 * rcn1) + (mb + ib * rcn2 * rcn2));
+      const V2 t = vperp(n);
+      float rct1 = vcross(r1, t), rct2 = vcross(r2, t);
+      C.tMass = 1.0f / ((ma + ia * rct1 * rct1) + (mb + ib * rct2 * rct2));
+      float dist = vdot(vadd(vsub(r2, r1), body_delta), n);
+      C.bias = -P.bias_coef * fminr(0.0f, dist + P.slop) / dt;
+      C.jb = 0.0f;
+      const V2 v1 = vadd(va, vmult(vperp(r1), wa));
+      const V2 v2s = vadd(vb, vmult(vperp(r2), wbv));
+      C.bounce = vdot(vsub(v2s, v1), n) * A.e;
+    }
+  }
+
+  // cpBodyUpdateVelocity + entities.py velocity_func (damping, max-velocity clamp)
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    const float mi = P.m_inv[b], ii = P.i_inv[b];
+    const float ffx = b < 4 ? fx[b] : 0.0f, ffy = b < 4 ? fy[b] : 0.0f, tt = b < 4 ? tq[b] : 0.0f;
+    float nvx = E.vx[b] * 1.0f + (0.0f + ffx * mi) * dt;
+    float nvy = E.vy[b] * 1.0f + (0.0f + ffy * mi) * dt;
+    float nw = E.w[b] * 1.0f + tt * ii * dt;
+    const float damp = b < 4 ? P.agent_damp : P.ball_damp;
+    nvx = nvx * damp;
+    nvy = nvy * damp;
+    if (b < 4) nw = nw * damp;
+    const float len = sqrtf(nvx * nvx + nvy * nvy);
+    if (len > P.vmax) {
+      nvx = (nvx / len) * P.vmax;
+      nvy = (nvy / len) * P.vmax;
+    }
+    L.v[SV_VX][b][lane] = nvx; L.v[SV_VY][b][lane] = nvy; L.v[SV_W][b][lane] = nw;
+  }
+
+  // cpArbiterApplyCachedImpulse
+  for (int k = 0; k < na; ++k) {
+    const Arb& A = arb[k];
+    if (!A.warm) continue;
+    const int ba = A.ba, bb = A.bb;
+    const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
+    const V2 n = v2(A.nx, A.ny);
+    for (int i = 0; i < A.count; ++i) {
+      const Contact& C = A.c[i];
+      const V2 j = vrotate(n, v2(C.jn, C.jt));
+      const V2 r1 = v2(C.r1x, C.r1y), r2 = v2(C.r2x, C.r2y);
+      const V2 nj = vneg(j);
+      L.v[SV_VX][ba][lane] = L.v[SV_VX][ba][lane] + nj.x * ma;
+      L.v[SV_VY][ba][lane] = L.v[SV_VY][ba][lane] + nj.y * ma;
+      L.v[SV_W][ba][lane] += ia * vcross(r1, nj);
+      L.v[SV_VX][bb][lane] = L.v[SV_VX][bb][lane] + j.x * mb;
+      L.v[SV_VY][bb][lane] = L.v[SV_VY][bb][lane] + j.y * mb;
+      L.v[SV_W][bb][lane] += ib * vcross(r2, j);
+    }
+  }
+
+  // cpArbiterApplyImpulse x 10
+#pragma unroll 1
+  for (int it = 0; it < 10; ++it) {
+    for (int k = 0; k < na; ++k) {
+      Arb& A = arb[k];
+      const int ba = A.ba, bb = A.bb;
+      const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
+      const V2 n = v2(A.nx, A.ny);
+      const float friction = A.u;
+      for (int i = 0; i < A.count; ++i) {
+        Contact& C = A.c[i];
+        const float nMass = C.nMass;
+        const V2 r1 = v2(C.r1x, C.r1y), r2 = v2(C.r2x, C.r2y);
+        const V2 vb1 = vadd(v2(L.v[SV_VBX][ba][lane], L.v[SV_VBY][ba][lane]), vmult(vperp(r1), L.v[SV_WB][ba][lane]));
+        const V2 vb2 = vadd(v2(L.v[SV_VBX][bb][lane], L.v[SV_VBY][bb][lane]), vmult(vperp(r2), L.v[SV_WB][bb][lane]));
+        const V2 vs1 = vadd(v2(L.v[SV_VX][ba][lane], L.v[SV_VY][ba][lane]), vmult(vperp(r1), L.v[SV_W][ba][lane]));
+        const V2 vs2 = vadd(v2(L.v[SV_VX][bb][lane], L.v[SV_VY][bb][lane]), vmult(vperp(r2), L.v[SV_W][bb][lane]));
+        const V2 vr = vsub(vs2, vs1);
+        const float vbn = vdot(vsub(vb2, vb1), n);
+        const float vrn = vdot(vr, n);
+        const float vrt = vdot(vr, vperp(n));
+
+        const float jbn = (C.bias - vbn) * nMass;
+        const float jbnOld = C.jb;
+        C.jb = fmaxr(jbnOld + jbn, 0.0f);
+
+        const float jn = -(C.bounce + vrn) * nMass;
+        const float jnOld = C.jn;
+        C.jn = fmaxr(jnOld + jn, 0.0f);
+
+        const float jtMax = friction * C.jn;
+        const float jt = -vrt * C.tMass;
+        const float jtOld = C.jt;
+        C.jt = fclamp(jtOld + jt, -jtMax, jtMax);
+
+        const V2 jbv = vmult(n, C.jb - jbnOld);
+        const V2 njb = vneg(jbv);
+        L.v[SV_VBX][ba][lane] = L.v[SV_VBX][ba][lane] + njb.x * ma;
+        L.v[SV_VBY][ba][lane] = L.v[SV_VBY][ba][lane] + njb.y * ma;
+        L.v[SV_WB][ba][lane] += ia * vcross(r1, njb);
+        L.v[SV_VBX][bb][lane] = L.v[SV_VBX][bb][lane] + jbv.x * mb;
+        L.v[SV_VBY][bb][lane] = L.v[SV_VBY][bb][lane] + jbv.y * mb;
+        L.v[SV_WB][bb][lane] += ib * vcross(r2, jbv);
+
+        const V2 j = vrotate(n, v2(C.jn - jnOld, C.jt - jtOld));
+        const V2 nj = vneg(j);
+        L.v[SV_VX][ba][lane] = L.v[SV_VX][ba][lane] + nj.x * ma;
+        L.v[SV_VY][ba][lane] = L.v[SV_VY][ba][lane] + nj.y * ma;
+        L.v[SV_W][ba][lane] += ia * vcross(r1, nj);
+        L.v[SV_VX][bb][lane] = L.v[SV_VX][bb][lane] + j.x * mb;
+        L.v[SV_VY][bb][lane] = L.v[SV_VY][bb][lane] + j.y * mb;
+        L.v[SV_W][bb][lane] += ib * vcross(r2, j);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    E.vx[b] = L.v[SV_VX][b][lane]; E.vy[b] = L.v[SV_VY][b][lane]; E.w[b] = L.v[SV_W][b][lane];
+    E.vbx[b] = L.v[SV_VBX][b][lane]; E.vby[b] = L.v[SV_VBY][b][lane]; E.wb[b] = L.v[SV_WB][b][lane];
+  }
+
+  // cpSpaceArbiterSetFilter: merge touched arbiters (idle 0) with aged old entries into the
+  // other cache buffer; entries idle for 3 steps are dropped.
+  const int npar = par ^ 1;
+  int nn = 0, ia = 0, ic = 0;
+  uint32_t ch = nc > 0 ? S.CH[(int64_t)(par * MAXA + 0) * S.n + e] : 0xffffffffu;
+  while (ia < na || ic < nc) {
+    const int pa = ia < na ? arb[ia].pair : (1 << 30);
+    const int pc = ic < nc ? (int)(ch & 63u) : (1 << 30);
+    uint32_t hdr;
+    float j4[4];
+    if (pa <= pc) {
+      const Arb& A = arb[ia];
+      hdr = (uint32_t)A.pair | ((uint32_t)A.count << 6);
+      hdr |= (uint32_t)(A.c[0].hash & 0xff) << 16;
+      if (A.count > 1) hdr |= (uint32_t)(A.c[1].hash & 0xff) << 24;
+      j4[0] = A.c[0].jn; j4[1] = A.c[0].jt;
+      j4[2] = A.count > 1 ? A.c[1].jn : 0.0f;
+      j4[3] = A.count > 1 ? A.c[1].jt : 0.0f;
+      ++ia;
+      if (pa == pc) {
+        ++ic;
+        ch = ic < nc ? S.CH[(int64_t)(par * MAXA + ic) * S.n + e] : 0xffffffffu;
+      }
+    } else {
+      const uint32_t idle = ((ch >> 8) & 3u) + 1u;
+      hdr = (ch & ~(3u << 8)) | (idle << 8);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) j4[f] = cache_field(S, par, ic, f, e);
+      ++ic;
+      ch = ic < nc ? S.CH[(int64_t)(par * MAXA + ic) * S.n + e] : 0xffffffffu;
+      if (idle >= 3u) continue;
+    }
+    if (nn >= MAXA) { (*overflow_acc)++; continue; }
+    S.CH[(int64_t)(npar * MAXA + nn) * S.n + e] = hdr;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) S.CJ[((int64_t)(npar * MAXA + nn) * 4 + f) * S.n + e] = j4[f];
+    ++nn;
+  }
+  E.meta = (E.meta & ~((63u << 8) | META_PAR)) | ((uint32_t)nn << 8) | (npar ? META_PAR : 0u);
+}
+
+// ---- kernels ---------------------------------------------------------------------------------
+__device__ __forceinline__ void load_scalars(const DevState& S, int64_t e, Env& E) {
+  const int64_t n = S.n;
+  E.steps = S.I[I_STEPS * n + e];
+  const uint32_t sc = (uint32_t)S.I[I_SCORE * n + e];
+  E.score_blue = (int)(sc & 0xffffu);
+  E.score_red = (int)(sc >> 16);
+  E.meta = (uint32_t)S.I[I_META * n + e];
+}
+__device__ __forceinline__ void store_scalars(const DevState& S, int64_t e, const Env& E) {
+  const int64_t n = S.n;
+  S.I[I_STEPS * n + e] = E.steps;
+  S.I[I_SCORE * n + e] = (int32_t)(((uint32_t)E.score_blue & 0xffffu) | ((uint32_t)E.score_red << 16));
+  S.I[I_META * n + e] = (int32_t)E.meta;
+}
+
+__global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P, const float* __restrict__ actions,
+                                                           float* __restrict__ obs, float* __restrict__ rew,
+                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                           int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
+                                                           Counters* ctr) {
+  __shared__ Lds L;
+  const int lane = threadIdx.x;
+  const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + lane;
+  if (e >= S.n) return;
+
+  // SoccerEnv.step validation + clip + fp32 scaling (soccer_env.py:101-125)
+  float a[12];
+  const float4* ap = (const float4*)(actions + e * 12);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    float4 v = ap[q];
+    a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+  }
+  bool finite = true;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) finite = finite && isfinite(a[k]);
+  if (!finite) {
+    atomicAdd(&ctr->nonfinite, 1ULL);
+    atomicMin(&ctr->first_bad, (long long)e);
+    return;
+  }
+  float fx[4], fy[4], tq[4];
+  Env E;
+  load_scalars(S, e, E);
+  load_bodies(S, e, E);
+  float pvx[5], pvy[5];
+#pragma unroll
+  for (int b = 0; b < 5; ++b) { pvx[b] = E.px[b]; pvy[b] = E.py[b]; }
+  E.steps += 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float F[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float v = a[i * 3 + k];
+      v = v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v);
+      F[k] = v * (k < 2 ? P.force_max : P.torque_max);
+    }
+    float s, c;
+    sincos_contract(E.ang[i], &s, &c);
+    fx[i] = 0.0f + (c * F[0] + (-s) * F[1]);
+    fy[i] = 0.0f + (s * F[0] + c * F[1]);
+    tq[i] = F[2];
+  }
+  unsigned long long ovf = 0;
+  physics_step(S, P, e, E, fx, fy, tq, L, lane, &ovf);
+  if (ovf) atomicAdd(&ctr->overflow, ovf);
+
+  // goal detection (game.py:401-412)
+  int goal = 0;
+  const float bx = E.px[4], by = E.py[4];
+  if (bx < 10.0f && 225.0f < by && by < 375.0f) { goal = 2; E.score_red += 1; }
+  else if (bx > 790.0f && 225.0f < by && by < 375.0f) { goal = 1; E.score_blue += 1; }
+  const bool done = P.max_steps > 0 && E.steps >= P.max_steps;
+  float r = blue_reward(P, pvx, pvy, E.px, E.py, goal, false, 0, 0);
+  bool rng_dirty = false;
+  if (goal) {
+    load_rng(S, e, E);
+    rng_dirty = true;
+    soft_reset_regs(E);
+  }
+  if (done) r = blue_reward(P, pvx, pvy, E.px, E.py, goal, true, E.score_blue, E.score_red);
+
+  // outputs of this step (before a vec auto-reset)
+  if (rew) *(float4*)(rew + e * 4) = make_float4(r, r, 0.0f, 0.0f);
+  if (term) *(uint32_t*)(term + e * 4) = 0u;
+  if (trunc) *(uint32_t*)(trunc + e * 4) = done ? 0x01010101u : 0u;
+  if (goal_out) goal_out[e] = (int8_t)goal;
+  if (score_out) *(int2*)(score_out + e * 2) = make_int2(E.score_blue, E.score_red);
+
+  if (done && P.autoreset) {
+    // marl_vecenv.py:48-51: env.reset(options={"use_full_random_positions": True})
+    if (!rng_dirty) load_rng(S, e, E);
+    rng_dirty = true;
+    reset_env_regs(E, MS_SPAWN_FULL_RANDOM);
+    emit_frames(S, P, e, E, true, obs);
+  } else {
+    emit_frames(S, P, e, E, (E.meta & META_HE) != 0, obs);
+  }
+  if (rng_dirty) store_rng(S, e, E);
+  store_bodies(S, e, E);
+  store_scalars(S, e, E);
+}
+
+__global__ __launch_bounds__(MS_BLOCK) void ms_reset_kernel(DevState S, Params P, const uint64_t* __restrict__ pcg,
+                                                            const uint8_t* __restrict__ mask, int mode, int set_hist_empty,
+                                                            float* __restrict__ obs) {
+  const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + threadIdx.x;
+  if (e >= S.n) return;
+  if (mask && !mask[e]) return;
+  Env E;
+  load_scalars(S, e, E);
+  if (pcg) {
+    E.rng.shi = pcg[e * 4 + 0]; E.rng.slo = pcg[e * 4 + 1];
+    E.rng.ihi = pcg[e * 4 + 2]; E.rng.ilo = pcg[e * 4 + 3];
+    E.rng.has32 = 0; E.rng.u32 = 0;
+  } else {
+    load_rng(S, e, E);
+  }
+  reset_env_regs(E, mode);
+  emit_frames(S, P, e, E, true, obs);
+  if (set_hist_empty) E.meta |= META_HE;
+  store_rng(S, e, E);
+  store_bodies(S, e, E);
+  store_scalars(S, e, E);
+}
+
+__global__ __launch_bounds__(MS_BLOCK) void ms_observe_kernel(DevState S, Params P, float* __restrict__ frames) {
+  const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + threadIdx.x;
+  if (e >= S.n) return;
+  Env E;
+  load_scalars(S, e, E);
+  load_bodies(S, e, E);
+#pragma unroll 1
+  for (int a = 0; a < 4; ++a) {
+    float f[22];
+    frame_of(P, E, a, f);
+#pragma unroll
+    for (int k = 0; k < 22; ++k) frames[e * 88 + a * 22 + k] = f[k];
+  }
+}
+
+__global__ void ms_export_kernel(DevState S, ms_env_state* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.n) return;
+  const int64_t n = S.n;
+  Env E;
+  load_scalars(S, e, E);
+  load_bodies(S, e, E);
+  load_rng(S, e, E);
+  ms_env_state& o = out[e];
+  for (int b = 0; b < 5; ++b) {
+    ms_body_state& d = o.body[b];
+    d.px = E.px[b]; d.py = E.py[b]; d.vx = E.vx[b]; d.vy = E.vy[b];
+    d.angle = b < 4 ? E.ang[b < 4 ? b : 0] : 0.0f;
+    d.w = E.w[b]; d.vbx = E.vbx[b]; d.vby = E.vby[b]; d.wb = E.wb[b];
+  }
+  const int head = (E.meta & META_RING) ? 1 : 0;
+  for (int a = 0; a < 4; ++a)
+    for (int k = 0; k < 22; ++k) {
+      o.frames[0][a][k] = S.F[(int64_t)(F_HIST + (head ^ 1) * 88 + a * 22 + k) * n + e];
+      o.frames[1][a][k] = S.F[(int64_t)(F_HIST + head * 88 + a * 22 + k) * n + e];
+    }
+  o.steps = E.steps; o.score_blue = E.score_blue; o.score_red = E.score_red;
+  o.mode = (uint8_t)META_MODE(E.meta);
+  o.hist_empty = (E.meta & META_HE) ? 1 : 0;
+  o.has_uint32 = E.rng.has32 ? 1 : 0;
+  o.uinteger = E.rng.u32;
+  o.pad = 0;
+  o.pcg_state_hi = E.rng.shi; o.pcg_state_lo = E.rng.slo;
+  o.pcg_inc_hi = E.rng.ihi; o.pcg_inc_lo = E.rng.ilo;
+  const int par = (E.meta & META_PAR) ? 1 : 0;
+  const int nc = META_NC(E.meta);
+  o.n_arb = (uint8_t)nc;
+  for (int k = 0; k < MAXA; ++k) {
+    ms_arbiter_state& A = o.arb[k];
+    memset(&A, 0, sizeof(A));
+    if (k >= nc) continue;
+    const uint32_t h = S.CH[(int64_t)(par * MAXA + k) * n + e];
+    A.pair = h & 63u; A.count = (h >> 6) & 3u; A.idle = (h >> 8) & 3u;
+    A.hash[0] = (h >> 16) & 0xffu; A.hash[1] = (h >> 24) & 0xffu;
+    A.jn[0] = cache_field(S, par, k, 0, e); A.jt[0] = cache_field(S, par, k, 1, e);
+    A.jn[1] = cache_field(S, par, k, 2, e); A.jt[1] = cache_field(S, par, k, 3, e);
+  }
+}
+
+__global__ void ms_import_kernel(DevState S, const ms_env_state* __restrict__ in) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.n) return;
+  const int64_t n = S.n;
+  const ms_env_state& o = in[e];
+  Env E;
+  for (int b = 0; b < 5; ++b) {
+    const ms_body_state& d = o.body[b];
+    E.px[b] = d.px; E.py[b] = d.py; E.vx[b] = d.vx; E.vy[b] = d.vy;
+    if (b < 4) E.ang[b] = d.angle;
+    E.w[b] = d.w; E.vbx[b] = d.vbx; E.vby[b] = d.vby; E.wb[b] = d.wb;
+  }
+  E.steps = o.steps; E.score_blue = o.score_blue; E.score_red = o.score_red;
+  const int nc = o.n_arb > MAXA ? MAXA : o.n_arb;
+  E.meta = (uint32_t)(o.mode & 3) | (o.hist_empty ? META_HE : 0u) | ((uint32_t)nc << 8) | (o.has_uint32 ? META_H32 : 0u);
+  E.rng.shi = o.pcg_state_hi; E.rng.slo = o.pcg_state_lo; E.rng.ihi = o.pcg_inc_hi; E.rng.ilo = o.pcg_inc_lo;
+  E.rng.has32 = o.has_uint32; E.rng.u32 = o.uinteger;
+  for (int a = 0; a < 4; ++a)
+    for (int k = 0; k < 22; ++k) {
+      S.F[(int64_t)(F_HIST + 0 * 88 + a * 22 + k) * n + e] = o.frames[0][a][k];  // ring head = 1
+      S.F[(int64_t)(F_HIST + 1 * 88 + a * 22 + k) * n + e] = o.frames[1][a][k];
+    }
+  E.meta |= META_RING;
+  for (int k = 0; k < nc; ++k) {
+    const ms_arbiter_state& A = o.arb[k];
+    S.CH[(int64_t)k * n + e] = (uint32_t)(A.pair & 63u) | ((uint32_t)(A.count & 3u) << 6) | ((uint32_t)(A.idle & 3u) << 8) |
+                               ((uint32_t)A.hash[0] << 16) | ((uint32_t)A.hash[1] << 24);
+    S.CJ[((int64_t)k * 4 + 0) * n + e] = A.jn[0];
+    S.CJ[((int64_t)k * 4 + 1) * n + e] = A.jt[0];
+    S.CJ[((int64_t)k * 4 + 2) * n + e] = A.jn[1];
+    S.CJ[((int64_t)k * 4 + 3) * n + e] = A.jt[1];
+  }
+  store_rng(S, e, E);
+  store_bodies(S, e, E);
+  store_scalars(S, e, E);
+}
+
+__global__ void ms_debug_rewards_kernel(Params P, int64_t n, const float* __restrict__ prev, const float* __restrict__ cur,
+                                        const int8_t* __restrict__ goal, const uint8_t* __restrict__ terminal,
+                                        const int32_t* __restrict__ score, float* __restrict__ rew) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  float pvx[5], pvy[5], cux[5], cuy[5];
+  for (int b = 0; b < 5; ++b) {
+    pvx[b] = prev[e * 10 + 2 * b]; pvy[b] = prev[e * 10 + 2 * b + 1];
+    cux[b] = cur[e * 10 + 2 * b]; cuy[b] = cur[e * 10 + 2 * b + 1];
+  }
+  const float r = blue_reward(P, pvx, pvy, cux, cuy, goal[e], terminal[e] != 0, score[2 * e], score[2 * e + 1]);
+  rew[2 * e] = r;
+  rew[2 * e + 1] = r;
+}
+
+// =============================================================================================
+// Host side: the C-ABI
+// =============================================================================================
+struct ms_env {
+  int device;
+  hipStream_t stream;
+  int64_t n;
+  Params P;
+  DevState S;
+  void* mem;
+  Counters* ctr;
+  ms_config cfg;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                                      \
+  do {                                                                                                 \
+    hipError_t _e = (x);                                                                               \
+    if (_e != hipSuccess) return fail(MS_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(_e));     \
+  } while (0)
+
+extern "C" {
+
+const char* ms_last_error(void) { return g_err.c_str(); }
+int ms_abi_version(void) { return MS_ABI_VERSION; }
+
+void ms_config_default(ms_config* c) {
+  memset(c, 0, sizeof(*c));
+  c->max_velocity = 200; c->agent_mass = 10; c->ball_mass = 1; c->agent_moment = 100;
+  c->ball_moment = 10; c->agent_friction = 0.99; c->ball_friction = 0.97;
+  c->agent_elasticity = 0.2; c->agent_surface_friction = 0.8; c->ball_elasticity = 0.95;
+  c->ball_surface_friction = 0.2; c->action_force_max = 150000.0; c->action_torque_max = 1000.0;
+  c->max_angular_velocity = 1000.0 / 100.0;
+  c->ball_proximity_multiplier = 0.002; c->move_ball_to_goal_multiplier = 0.1;
+  c->alive_penalty = 0.00001; c->goal_scored_reward = 4.0; c->goal_conceded_penalty = 0.0;
+  c->score_difference_multiplier = 0.0; c->max_steps = 1000; c->autoreset = 1;
+}
+
+// --- numpy SeedSequence (bit_generator.pyx) -> PCG64 seeding (pcg64.c pcg64_set_seed) ------
+static void seed_sequence_pcg64(const uint32_t* entropy, int n_words, uint64_t out[4]) {
+  const uint32_t INIT_A = 0x43b0d7e5u, MULT_A = 0x931e8875u, INIT_B = 0x8b51f9ddu, MULT_B = 0x58f38dedu;
+  const uint32_t MIX_MULT_L = 0xca01f9ddu, MIX_MULT_R = 0x4973f715u;
+  uint32_t pool[4];
+  uint32_t hash_const = INIT_A;
+  auto hashmix = [&](uint32_t value) {
+    value ^= hash_const;
+    hash_const *= MULT_A;
+    value *= hash_const;
+    value ^= value >> 16;
+    return value;
+  };
+  auto mix = [](uint32_t x, uint32_t y) {
+    uint32_t result = MIX_MULT_L * x - MIX_MULT_R * y;
+    result ^= result >> 16;
+    return result;
+  };
+  for (int i = 0; i < 4; ++i) pool[i] = hashmix(i < n_words ? entropy[i] : 0u);
+  for (int s = 0; s < 4; ++s)
+    for (int d = 0; d < 4; ++d)
+      if (s != d) pool[d] = mix(pool[d], hashmix(pool[s]));
+  for (int s = 4; s < n_words; ++s)
+    for (int d = 0; d < 4; ++d) pool[d] = mix(pool[d], hashmix(entropy[s]));
+  uint32_t words[8];
+  uint32_t hc = INIT_B;
+  for (int i = 0; i < 8; ++i) {
+    uint32_t v = pool[i % 4];
+    v ^= hc;
+    hc *= MULT_B;
+    v *= hc;
+    v ^= v >> 16;
+    words[i] = v;
+  }
+  uint64_t v[4];
+  for (int i = 0; i < 4; ++i) v[i] = (uint64_t)words[2 * i] | ((uint64_t)words[2 * i + 1] << 32);
+  // pcg64_set_seed(seed = v[0:2], inc = v[2:4]); PCG_128BIT_CONSTANT(high, low)
+  typedef unsigned __int128 u128;
+  const u128 MULT = ((u128)0x2360ED051FC65DA4ULL << 64) | 0x4385DF649FCCF645ULL;
+  u128 initstate = ((u128)v[0] << 64) | v[1];
+  u128 initseq = ((u128)v[2] << 64) | v[3];
+  u128 inc = (initseq << 1) | 1u;
+  u128 st = 0;
+  st = st * MULT + inc;
+  st += initstate;
+  st = st * MULT + inc;
+  out[0] = (uint64_t)(st >> 64); out[1] = (uint64_t)st;
+  out[2] = (uint64_t)(inc >> 64); out[3] = (uint64_t)inc;
+}
+
+int ms_seed_pcg64(const uint32_t* entropy, int n_words, uint64_t out[4]) {
+  if (!entropy || n_words < 1 || !out) return fail(MS_ERR_INVALID_ARGUMENT, "ms_seed_pcg64: bad arguments");
+  seed_sequence_pcg64(entropy, n_words, out);
+  return MS_OK;
+}
+
+int ms_seed_pcg64_range(uint64_t seed0, int64_t n, uint64_t* out) {
+  if (!out || n < 0) return fail(MS_ERR_INVALID_ARGUMENT, "ms_seed_pcg64_range: bad arguments");
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t s = seed0 + (uint64_t)i;
+    uint32_t w[2] = {(uint32_t)s, (uint32_t)(s >> 32)};
+    seed_sequence_pcg64(w, w[1] ? 2 : 1, out + 4 * i);
+  }
+  return MS_OK;
+}
+
+// --- parameter setup: identical float arithmetic to oracle orc_params_init (ORC_F32) -------
+static void make_params(const ms_config* cfg, Params* P) {
+  memset(P, 0, sizeof(*P));
+  P->dt = (float)(1.0 / 60.0);
+  P->bias_coef = (float)(1.0 - pow(pow(1.0 - 0.1, 60.0), 1.0 / 60.0));
+  P->slop = 0.1f;
+  const float am = (float)cfg->agent_mass, bm = (float)cfg->ball_mass;
+  const float ai = (float)cfg->agent_moment, bi = (float)cfg->ball_moment;
+  for (int i = 0; i < 4; ++i) { P->m_inv[i] = 1.0f / am; P->i_inv[i] = 1.0f / ai; }
+  P->m_inv[4] = 1.0f / bm; P->i_inv[4] = 1.0f / bi;
+  P->m_inv[5] = 0.0f; P->i_inv[5] = 0.0f;
+  P->agent_damp = (float)cfg->agent_friction;
+  P->ball_damp = (float)cfg->ball_friction;
+  P->vmax = (float)cfg->max_velocity;
+  P->force_max = (float)cfg->action_force_max;
+  P->torque_max = (float)cfg->action_torque_max;
+  P->obs_vmax = (float)(cfg->max_velocity > 1e-6 ? cfg->max_velocity : 1e-6);
+  P->obs_wmax = (float)(cfg->max_angular_velocity > 1e-6 ? cfg->max_angular_velocity : 1e-6);
+  const float ea = (float)cfg->agent_elasticity, ua = (float)cfg->agent_surface_friction;
+  const float eb = (float)cfg->ball_elasticity, ub = (float)cfg->ball_surface_friction;
+  const float ew = 0.95f, uw = 0.2f, eg = 0.95f, ug = 0.0f;
+  P->e_aa = ea * ea; P->u_aa = ua * ua;
+  P->e_ab = eb * ea; P->u_ab = ub * ua;
+  P->e_aw = ew * ea; P->u_aw = uw * ua;
+  P->e_ag = eg * ea; P->u_ag = ug * ua;
+  P->e_bw = eb * ew; P->u_bw = ub * uw;
+  P->prox_mult = (float)cfg->ball_proximity_multiplier;
+  P->goal_mult = (float)cfg->move_ball_to_goal_multiplier;
+  P->alive = (float)cfg->alive_penalty;
+  P->goal_reward = (float)cfg->goal_scored_reward;
+  P->concede_penalty = (float)cfg->goal_conceded_penalty;
+  P->score_diff_mult = (float)cfg->score_difference_multiplier;
+  P->max_steps = cfg->max_steps;
+  P->autoreset = cfg->autoreset;
+  static const double DEF[8][5] = {{10, 10, 790, 10, 2},   {10, 590, 790, 590, 2}, {10, 10, 10, 225, 2},
+                                   {10, 375, 10, 590, 2},  {790, 10, 790, 225, 2}, {790, 375, 790, 590, 2},
+                                   {10, 225, 10, 375, 1},  {790, 225, 790, 375, 1}};
+  for (int s = 0; s < 8; ++s) {
+    Seg& g = P->seg[s];
+    g.ax = (float)DEF[s][0]; g.ay = (float)DEF[s][1]; g.bx = (float)DEF[s][2]; g.by = (float)DEF[s][3];
+    g.r = (float)DEF[s][4];
+    const float dx = g.bx - g.ax, dy = g.by - g.ay;
+    const float len = sqrtf(dx * dx + dy * dy);
+    const float inv = 1.0f / (len + 1.17549435082228750797e-38f);
+    const float ux = dx * inv, uy = dy * inv;
+    g.nx = -uy; g.ny = ux;
+    float l, r, bt, t;
+    if (g.ax < g.bx) { l = g.ax; r = g.bx; } else { l = g.bx; r = g.ax; }
+    if (g.ay < g.by) { bt = g.ay; t = g.by; } else { bt = g.by; t = g.ay; }
+    g.bb[0] = l - g.r; g.bb[1] = bt - g.r; g.bb[2] = r + g.r; g.bb[3] = t + g.r;
+  }
+}
+
+static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms_env** out) {
+  if (!out || n_envs <= 0) return fail(MS_ERR_INVALID_ARGUMENT, "ms_create: n_envs must be > 0");
+  if (n_envs > ((int64_t)1 << 31)) return fail(MS_ERR_INVALID_ARGUMENT, "ms_create: n_envs too large");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MS_ERR_NO_DEVICE, "ms_create: no HIP device");
+  if (device < 0 || device >= ndev) return fail(MS_ERR_INVALID_ARGUMENT, "ms_create: bad device index");
+  HIPCHK(hipSetDevice(device));
+  ms_env* h = new ms_env();
+  h->device = device;
+  h->stream = (hipStream_t)stream;
+  h->n = n_envs;
+  if (cfg) h->cfg = *cfg; else ms_config_default(&h->cfg);
+  make_params(&h->cfg, &h->P);
+  const size_t n = (size_t)n_envs;
+  const size_t bytes_F = sizeof(float) * PL_F * n;
+  const size_t bytes_I = sizeof(int32_t) * PL_I * n;
+  const size_t bytes_R = sizeof(uint64_t) * 4 * n;
+  const size_t bytes_CH = sizeof(uint32_t) * 2 * MAXA * n;
+  const size_t bytes_CJ = sizeof(float) * 2 * MAXA * 4 * n;
+  const size_t total = bytes_R + bytes_F + bytes_I + bytes_CH + bytes_CJ + 256;
+  char* base = nullptr;
+  if (hipMalloc((void**)&base, total) != hipSuccess) {
+    delete h;
+    return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of device state failed");
+  }
+  h->mem = base;
+  h->S.R = (uint64_t*)base; base += bytes_R;
+  h->S.F = (float*)base; base += bytes_F;
+  h->S.I = (int32_t*)base; base += bytes_I;
+  h->S.CH = (uint32_t*)base; base += bytes_CH;
+  h->S.CJ = (float*)base; base += bytes_CJ;
+  h->S.n = n_envs;
+  if (hipMalloc((void**)&h->ctr, sizeof(Counters)) != hipSuccess) {
+    (void)hipFree(h->mem);
+    delete h;
+    return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of counters failed");
+  }
+  HIPCHK(hipMemsetAsync(h->mem, 0, total, h->stream));
+  Counters c0 = {0, 0, (long long)INT64_MAX};
+  HIPCHK(hipMemcpyAsync(h->ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, h->stream));
+  // Game.__init__: entropy-seeded default_rng() + reset() (game.py:17, 74)
+  uint64_t* hp = (uint64_t*)malloc(sizeof(uint64_t) * 4 * n);
+  std::random_device rd;
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t w[4] = {rd(), rd(), rd(), rd()};
+    seed_sequence_pcg64(w, 4, hp + 4 * i);
+  }
+  uint64_t* dp = nullptr;
+  if (hipMalloc((void**)&dp, sizeof(uint64_t) * 4 * n) != hipSuccess) {
+    free(hp);
+    return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of seed buffer failed");
+  }
+  HIPCHK(hipMemcpyAsync(dp, hp, sizeof(uint64_t) * 4 * n, hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(ms_reset_kernel, dim3(grid_for(n_envs, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S, h->P,
+                     (const uint64_t*)dp, (const uint8_t*)nullptr, (int)MS_SPAWN_RANDOM, 1, (float*)nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(h->stream));
+  (void)hipFree(dp);
+  free(hp);
+  *out = h;
+  return MS_OK;
+}
+
+int ms_destroy(ms_env* h) {
+  if (!h) return MS_OK;
+  (void)hipSetDevice(h->device);
+  (void)hipStreamSynchronize(h->stream);
+  (void)hipFree(h->mem);
+  (void)hipFree(h->ctr);
+  delete h;
+  return MS_OK;
+}
+
+int ms_set_stream(ms_env* h, void* stream) {
+  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_stream: null handle");
+  h->stream = (hipStream_t)stream;
+  return MS_OK;
+}
+
+int64_t ms_num_envs(const ms_env* h) { return h ? h->n : -1; }
+
+int ms_reset(ms_env* h, const uint64_t* pcg, const uint8_t* mask, int mode, float* obs) {
+  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_reset: null handle");
+  if (mode < 0 || mode > 2) return fail(MS_ERR_INVALID_ARGUMENT, "ms_reset: mode must be 0, 1 or 2");
+  hipLaunchKernelGGL(ms_reset_kernel, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S, h->P, pcg,
+                     mask, mode, 0, obs);
+  HIPCHK(hipGetLastError());
+  return MS_OK;
+}
+
+int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* term, uint8_t* trunc, int8_t* goal,
+            int32_t* score) {
+  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: null handle");
+  if (!actions || !obs) return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: actions and obs are required");
+  if (((uintptr_t)actions & 15u) || ((uintptr_t)obs & 7u) || ((uintptr_t)rew & 15u) || ((uintptr_t)term & 3u) ||
+      ((uintptr_t)trunc & 3u) || ((uintptr_t)score & 7u))
+    return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: misaligned buffer (actions/rew 16 B, obs/score 8 B, flags 4 B)");
+  hipLaunchKernelGGL(ms_step_kernel, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S, h->P,
+                     actions, obs, rew, term, trunc, goal, score, h->ctr);
+  HIPCHK(hipGetLastError());
+  return MS_OK;
+}
+
+int ms_observe(ms_env* h, float* frames) {
+  if (!h || !frames) return fail(MS_ERR_INVALID_ARGUMENT, "ms_observe: bad arguments");
+  hipLaunchKernelGGL(ms_observe_kernel, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S, h->P,
+                     frames);
+  HIPCHK(hipGetLastError());
+  return MS_OK;
+}
+
+int ms_export_state(ms_env* h, ms_env_state* dst) {
+  if (!h || !dst) return fail(MS_ERR_INVALID_ARGUMENT, "ms_export_state: bad arguments");
+  hipLaunchKernelGGL(ms_export_kernel, dim3(grid_for(h->n, 128)), dim3(128), 0, h->stream, h->S, dst);
+  HIPCHK(hipGetLastError());
+  return MS_OK;
+}
+
+int ms_import_state(ms_env* h, const ms_env_state* src) {
+  if (!h || !src) return fail(MS_ERR_INVALID_ARGUMENT, "ms_import_state: bad arguments");
+  hipLaunchKernelGGL(ms_import_kernel, dim3(grid_for(h->n, 128)), dim3(128), 0, h->stream, h->S, src);
+  HIPCHK(hipGetLastError());
+  return MS_OK;
+}
+
+int ms_debug_rewards(ms_env* h, const float* prev_pos, const float* cur_pos, const int8_t* goal,
+                     const uint8_t* terminal, const int32_t* score, float* rew) {
+  if (!h || !prev_pos || !cur_pos || !goal || !terminal || !score || !rew)
+    return fail(MS_ERR_INVALID_ARGUMENT, "ms_debug_rewards: bad arguments");
+  hipLaunchKernelGGL(ms_debug_rewards_kernel, dim3(grid_for(h->n, 128)), dim3(128), 0, h->stream, h->P, h->n,
+                     prev_pos, cur_pos, goal, terminal, score, rew);
+  HIPCHK(hipGetLastError());
+  return MS_OK;
+}
+
+int ms_get_stats(ms_env* h, ms_stats* out) {
+  if (!h || !out) return fail(MS_ERR_INVALID_ARGUMENT, "ms_get_stats: bad arguments");
+  Counters c;
+  HIPCHK(hipMemcpyAsync(&c, h->ctr, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  out->arbiter_overflow = c.overflow;
+  out->nonfinite_envs = c.nonfinite;
+  out->first_nonfinite_env = c.first_bad == (long long)INT64_MAX ? -1 : c.first_bad;
+  return MS_OK;
+}
+
+int ms_reset_stats(ms_env* h) {
+  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_reset_stats: null handle");
+  Counters c0 = {0, 0, (long long)INT64_MAX};
+  HIPCHK(hipMemcpyAsync(h->ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, h->stream));
+  return MS_OK;
+}
+
+}  // extern "C"

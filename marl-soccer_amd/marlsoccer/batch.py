@@ -1,0 +1,189 @@
+"""SoccerBatch: N soccer envs resident on one MI355X, stepped by one fused HIP kernel.
+
+This is the GPU-native form of the reference's batched boundary
+(SyncMultiAgentVecEnv over SoccerEnv over Game; marl_vecenv.py:3-80, soccer_env.py:16-171,
+game/game.py:10-437). Inputs and outputs are torch tensors on the env's device; nothing
+is copied to the host unless the caller asks.
+
+    batch = SoccerBatch(65536, device=0)
+    obs = batch.reset(seed=19)                       # (N, 4, 66) f32, seeds 19 + i
+    obs, rew, term, trunc, goal, score = batch.step(actions)   # actions (N, 4, 3) f32
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .config import resolve, to_ms_config
+
+MODE_BY_OPTION = {"use_fixed_positions": N.SPAWN_FIXED, "use_full_random_positions": N.SPAWN_FULL_RANDOM}
+
+
+def spawn_mode(options) -> int:
+    """SoccerEnv.reset options -> spawn mode (soccer_env.py:83-89, game.py:109-114)."""
+    if isinstance(options, dict):
+        if bool(options.get("use_fixed_positions", False)):
+            return N.SPAWN_FIXED
+        if bool(options.get("use_full_random_positions", False)):
+            return N.SPAWN_FULL_RANDOM
+    return N.SPAWN_RANDOM
+
+
+class StepOutput(tuple):
+    """(obs, rew, term, trunc, goal, score) device tensors."""
+
+    __slots__ = ()
+    obs = property(lambda s: s[0])
+    rew = property(lambda s: s[1])
+    term = property(lambda s: s[2])
+    trunc = property(lambda s: s[3])
+    goal = property(lambda s: s[4])
+    score = property(lambda s: s[5])
+
+
+class SoccerBatch:
+    """N independent 2v2 soccer envs on one HIP device.
+
+    autoreset=True gives SyncMultiAgentVecEnv semantics (a finished env restarts with the
+    full-random spawn inside step and returns its reset obs); autoreset=False gives
+    SoccerEnv semantics (the caller resets).
+    """
+
+    def __init__(self, num_envs: int, config: dict | None = None, device=None, autoreset: bool = True,
+                 stream: torch.cuda.Stream | None = None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("SoccerBatch needs a HIP device (MI355X); there is no CPU fallback")
+        self.config = resolve(config)
+        self.num_envs = int(num_envs)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   (device if isinstance(device, int) else torch.device(device).index or 0))
+        self.autoreset = bool(autoreset)
+        self._L = N.lib()
+        self._cfg = to_ms_config(self.config, self.autoreset)
+        with torch.cuda.device(self.device):
+            self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
+            h = C.c_void_p()
+            N.check(self._L.ms_create(C.byref(self._cfg), self.num_envs, self.device.index,
+                                      C.c_void_p(self.stream.cuda_stream), C.byref(h)), "ms_create")
+        self._h = h
+        n, dev = self.num_envs, self.device
+        self.obs = torch.zeros((n, 4, 66), dtype=torch.float32, device=dev)
+        self.rew = torch.zeros((n, 4), dtype=torch.float32, device=dev)
+        self.term = torch.zeros((n, 4), dtype=torch.uint8, device=dev)
+        self.trunc = torch.zeros((n, 4), dtype=torch.uint8, device=dev)
+        self.goal = torch.zeros((n,), dtype=torch.int8, device=dev)
+        self.score = torch.zeros((n, 2), dtype=torch.int32, device=dev)
+
+    # ---- lifecycle ---------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.ms_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order varies
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ptr(self, t: torch.Tensor | None):
+        if t is None:
+            return None
+        if t.device != self.device:
+            raise ValueError(f"tensor on {t.device}, env on {self.device}")
+        if not t.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return C.c_void_p(t.data_ptr())
+
+    # ---- API ---------------------------------------------------------------------------
+    def reset(self, seed=None, options=None, mask: torch.Tensor | None = None, out: torch.Tensor | None = None):
+        """Game.reset for every env (or the envs selected by `mask`).
+
+        seed: None (keep each env's RNG stream; reset(seed=None)), an int s (env i gets
+        default_rng(s + i), marl_vecenv.py:23) or an (N, 4) uint64 array of PCG64 states.
+        """
+        mode = spawn_mode(options)
+        pcg_t = None
+        if seed is not None:
+            if isinstance(seed, (int, np.integer)):
+                pcg = N.pcg_states_for_range(int(seed), self.num_envs)
+            else:
+                pcg = np.ascontiguousarray(seed, dtype=np.uint64).reshape(self.num_envs, 4)
+            pcg_t = torch.from_numpy(pcg.view(np.int64)).to(self.device)
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        obs = self.obs if out is None else out
+        with torch.cuda.device(self.device):
+            N.check(self._L.ms_reset(self._h, self._ptr(pcg_t), self._ptr(m), mode, self._ptr(obs)), "ms_reset")
+        return obs
+
+    def step(self, actions: torch.Tensor) -> StepOutput:
+        """One env.step for all envs; actions (N, 4, 3) float32 on the env's device."""
+        if actions.shape != (self.num_envs, 4, 3):
+            raise ValueError(f"actions must have shape ({self.num_envs}, 4, 3), got {tuple(actions.shape)}")
+        if actions.dtype != torch.float32:
+            actions = actions.float()
+        actions = actions.contiguous()
+        with torch.cuda.device(self.device):
+            N.check(self._L.ms_step(self._h, self._ptr(actions), self._ptr(self.obs), self._ptr(self.rew),
+                                    self._ptr(self.term), self._ptr(self.trunc), self._ptr(self.goal),
+                                    self._ptr(self.score)), "ms_step")
+        return StepOutput((self.obs, self.rew, self.term, self.trunc, self.goal, self.score))
+
+    def step_into(self, actions: torch.Tensor, obs: torch.Tensor, rew=None, term=None, trunc=None, goal=None,
+                  score=None) -> None:
+        """ms_step with caller-owned output tensors (any may be None except obs)."""
+        with torch.cuda.device(self.device):
+            N.check(self._L.ms_step(self._h, self._ptr(actions), self._ptr(obs), self._ptr(rew), self._ptr(term),
+                                    self._ptr(trunc), self._ptr(goal), self._ptr(score)), "ms_step")
+
+    def observe(self) -> torch.Tensor:
+        """Current frame of every agent, (N, 4, 22) (Game._get_observations)."""
+        out = torch.empty((self.num_envs, 4, 22), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            N.check(self._L.ms_observe(self._h, self._ptr(out)), "ms_observe")
+        return out
+
+    def export_state(self) -> np.ndarray:
+        """Full per-env state as a numpy ms_env_state record array (synchronises)."""
+        buf = torch.empty((self.num_envs, N.ENV_STATE_DTYPE.itemsize), dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            N.check(self._L.ms_export_state(self._h, self._ptr(buf)), "ms_export_state")
+        host = buf.cpu().numpy()
+        return host.view(N.ENV_STATE_DTYPE).reshape(self.num_envs)
+
+    def import_state(self, state: np.ndarray) -> None:
+        st = np.ascontiguousarray(state, dtype=N.ENV_STATE_DTYPE).reshape(self.num_envs)
+        buf = torch.from_numpy(st.view(np.uint8).reshape(self.num_envs, -1).copy()).to(self.device)
+        with torch.cuda.device(self.device):
+            N.check(self._L.ms_import_state(self._h, self._ptr(buf)), "ms_import_state")
+        self.synchronize()
+
+    def debug_rewards(self, prev_pos, cur_pos, goal, terminal, score) -> torch.Tensor:
+        d = self.device
+        pv = torch.as_tensor(np.ascontiguousarray(prev_pos, np.float32)).to(d)
+        cu = torch.as_tensor(np.ascontiguousarray(cur_pos, np.float32)).to(d)
+        g = torch.as_tensor(np.ascontiguousarray(goal, np.int8)).to(d)
+        t = torch.as_tensor(np.ascontiguousarray(terminal, np.uint8)).to(d)
+        s = torch.as_tensor(np.ascontiguousarray(score, np.int32)).to(d)
+        out = torch.empty((self.num_envs, 2), dtype=torch.float32, device=d)
+        with torch.cuda.device(self.device):
+            N.check(self._L.ms_debug_rewards(self._h, *(self._ptr(x) for x in (pv, cu, g, t, s, out))),
+                    "ms_debug_rewards")
+        return out
+
+    def stats(self) -> dict:
+        st = N.MsStats()
+        N.check(self._L.ms_get_stats(self._h, C.byref(st)), "ms_get_stats")
+        return {"arbiter_overflow": int(st.arbiter_overflow), "nonfinite_envs": int(st.nonfinite_envs),
+                "first_nonfinite_env": int(st.first_nonfinite_env)}
+
+    def reset_stats(self) -> None:
+        N.check(self._L.ms_reset_stats(self._h), "ms_reset_stats")
+
+    def synchronize(self) -> None:
+        self.stream.synchronize()

@@ -1,0 +1,258 @@
+"""GPU (HIP kernel through the C-ABI) vs the oracle — the parity tests proper.
+
+Bars:
+  - vs the fp32 oracle (the kernel's arithmetic contract): bit-exact for every output and
+    the full exported state, over trajectories that cross goals, soft resets, episode ends
+    and auto-resets. (The north-star 1e-5 fp32 tolerance is implied by equality.)
+  - vs the golden fixtures captured from the reference glue (identical input states):
+    spawn positions exact after fp32 rounding, PCG64 stream exact, observations within
+    1e-5, rewards within 1e-5 (+ fp32 relative rounding on synthetic teleports).
+"""
+import numpy as np
+import pytest
+
+import golden_io as gio
+import oracle as orc
+import sim_helpers as sh
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ms():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    import marlsoccer
+    return marlsoccer
+
+
+def cfg_dict(**over):
+    from marlsoccer.config import load_config
+    c = load_config()
+    for k, v in over.items():
+        sect = "simulation" if k == "max_steps" else ("physics" if k in c["physics"] else "rewards")
+        c[sect][k] = v
+    return c
+
+
+def oracle_cfg(ms_cfg):
+    o = orc.MsConfig()
+    for name, _ in ms_cfg._fields_:
+        setattr(o, name, getattr(ms_cfg, name))
+    return o
+
+
+def assert_state_equal(gpu_st, orc_st, where=""):
+    for f in ("steps", "score_blue", "score_red", "mode", "hist_empty", "n_arb", "has_uint32", "uinteger",
+              "pcg_state_hi", "pcg_state_lo", "pcg_inc_hi", "pcg_inc_lo"):
+        np.testing.assert_array_equal(gpu_st[f], orc_st[f], err_msg=f"{where} {f}")
+    for f in ("px", "py", "vx", "vy", "angle", "w", "vbx", "vby", "wb"):
+        np.testing.assert_array_equal(gpu_st["body"][f], orc_st["body"][f], err_msg=f"{where} body.{f}")
+    np.testing.assert_array_equal(gpu_st["frames"], orc_st["frames"], err_msg=f"{where} frames")
+    for i in range(len(gpu_st)):
+        k = int(orc_st["n_arb"][i])
+        for f in ("pair", "count", "idle", "hash", "jn", "jt"):
+            np.testing.assert_array_equal(gpu_st["arb"][f][i, :k], orc_st["arb"][f][i, :k],
+                                          err_msg=f"{where} env {i} arb.{f}")
+
+
+def run_pair(ms, n, steps, seed=19, mode_opts=None, chase=True, check_state_every=50, **over):
+    config = cfg_dict(**over)
+    gpu = ms.SoccerBatch(n, config=config, autoreset=True)
+    ocfg = oracle_cfg(ms.to_ms_config(config, True))
+    ref = orc.OracleBatch(n, "f32", ocfg)
+    mode = ms.spawn_mode(mode_opts)
+    pcg = np.stack([orc.pcg_from_seed(seed + i) for i in range(n)])
+    go = gpu.reset(seed=seed, options=mode_opts).cpu().numpy()
+    ro = ref.reset(pcg, mode)
+    np.testing.assert_array_equal(go, ro)
+    rng = np.random.default_rng(seed)
+    chaser = np.arange(n) % 4
+    counts = {"goals": 0, "dones": 0}
+    for t in range(steps):
+        if chase:
+            st = ref.export_state()
+            pos = np.stack([st["body"]["px"], st["body"]["py"]], -1)
+            act = sh.chase_actions(pos, st["body"]["angle"][:, :4], rng, chaser)
+        else:
+            act = sh.hash_actions(n, t)
+        out = gpu.step(torch.from_numpy(act).to(gpu.device))
+        obs, rew, trunc, goal, score, bad = ref.step(act)
+        assert bad == 0
+        g_obs = out.obs.cpu().numpy()
+        np.testing.assert_array_equal(out.goal.cpu().numpy(), goal, err_msg=f"goal t={t}")
+        np.testing.assert_array_equal(out.score.cpu().numpy(), score, err_msg=f"score t={t}")
+        np.testing.assert_array_equal(out.trunc.cpu().numpy().astype(bool), trunc, err_msg=f"trunc t={t}")
+        assert not out.term.cpu().numpy().any()
+        np.testing.assert_array_equal(out.rew.cpu().numpy(), rew.astype(np.float32), err_msg=f"rew t={t}")
+        np.testing.assert_array_equal(g_obs, obs, err_msg=f"obs t={t}")
+        counts["goals"] += int((goal != 0).sum())
+        counts["dones"] += int(trunc[:, 0].sum())
+        if check_state_every and (t % check_state_every == check_state_every - 1 or t == steps - 1):
+            assert_state_equal(gpu.export_state(), ref.export_state(), f"t={t}")
+    assert gpu.stats()["arbiter_overflow"] == 0 and ref.overflow() == 0
+    gpu.close()
+    return counts
+
+
+def test_reset_modes_bitexact(ms):
+    for opts in (None, {"use_full_random_positions": True}, {"use_fixed_positions": True}):
+        n = 300
+        gpu = ms.SoccerBatch(n)
+        ref = orc.OracleBatch(n, "f32")
+        pcg = np.stack([orc.pcg_from_seed(7 + i) for i in range(n)])
+        go = gpu.reset(seed=7, options=opts).cpu().numpy()
+        ro = ref.reset(pcg, ms.spawn_mode(opts))
+        np.testing.assert_array_equal(go, ro)
+        assert_state_equal(gpu.export_state(), ref.export_state(), str(opts))
+        gpu.close()
+
+
+def test_trajectory_chase_bitexact(ms):
+    c = run_pair(ms, 128, 1100, seed=19)
+    assert c["goals"] > 10 and c["dones"] == 128, c
+
+
+def test_trajectory_random_bitexact(ms):
+    run_pair(ms, 256, 400, seed=3, chase=False, check_state_every=100)
+
+
+def test_short_episodes_full_random_bitexact(ms):
+    c = run_pair(ms, 96, 500, seed=5, mode_opts={"use_full_random_positions": True}, max_steps=70,
+                 score_difference_multiplier=5.0, goal_conceded_penalty=1.0)
+    assert c["dones"] >= 96 * 7 and c["goals"] > 0, c
+
+
+def test_fixed_spawn_no_truncation_bitexact(ms):
+    run_pair(ms, 64, 600, seed=11, mode_opts={"use_fixed_positions": True}, max_steps=0)
+
+
+# ---- golden fixtures (reference glue) through the GPU path --------------------------------
+
+def test_gpu_spawn_matches_reference_fixture(ms):
+    fx = gio.load("spawn.npz")
+    n = len(fx["seed"])
+    gpu = ms.SoccerBatch(n)
+    for mode in (0, 1, 2):
+        sel = fx["mode"] == mode
+        pcg = np.zeros((n, 4), np.uint64)
+        pcg[:] = fx["pcg0"]
+        mask = torch.from_numpy(sel.astype(np.uint8))
+        gpu.reset(seed=pcg, options=[None, {"use_full_random_positions": True}, {"use_fixed_positions": True}][mode],
+                  mask=mask)
+    st = gpu.export_state()
+    pos = np.stack([st["body"]["px"], st["body"]["py"]], -1)
+    np.testing.assert_array_equal(pos, fx["pos"][:, 0].astype(np.float32))
+    rng = np.stack([st["pcg_state_hi"], st["pcg_state_lo"], st["pcg_inc_hi"], st["pcg_inc_lo"],
+                    st["has_uint32"].astype(np.uint64), st["uinteger"].astype(np.uint64)], -1)
+    np.testing.assert_array_equal(rng, fx["rng"][:, 0])
+    np.testing.assert_array_equal(st["body"]["angle"][:, :4], fx["angle"][:, 0].astype(np.float32))
+    gpu.close()
+
+
+def test_gpu_observations_match_reference_fixture(ms):
+    fx = gio.load("obs.npz")
+    n = len(fx["frames"])
+    st = np.zeros((n,), orc.ENV_STATE_DTYPE)
+    st["body"]["px"] = fx["pos"][..., 0]
+    st["body"]["py"] = fx["pos"][..., 1]
+    st["body"]["vx"] = fx["vel"][..., 0]
+    st["body"]["vy"] = fx["vel"][..., 1]
+    st["body"]["angle"][:, :4] = fx["angle"]
+    st["body"]["w"][:, :4] = fx["w"]
+    gpu = ms.SoccerBatch(n)
+    gpu.import_state(st)
+    got = gpu.observe().cpu().numpy()
+    np.testing.assert_allclose(got, fx["frames"], rtol=0, atol=1e-5)
+    ref = orc.OracleBatch(n, "f32")
+    ref.import_state(st)
+    np.testing.assert_array_equal(got, ref.observe())
+    gpu.close()
+
+
+@pytest.mark.parametrize("variant", ["default", "conceded"])
+def test_gpu_rewards_match_reference_fixture(ms, variant):
+    fx = gio.load("rewards.npz")
+    n = len(fx["goal"])
+    over = {} if variant == "default" else {"goal_conceded_penalty": 1.5, "ball_proximity_multiplier": 0.0}
+    gpu = ms.SoccerBatch(n, config=cfg_dict(**over))
+    got = gpu.debug_rewards(fx["prev"], fx["cur"], fx["goal"], np.zeros(n, np.uint8),
+                            np.zeros((n, 2), np.int32)).cpu().numpy()
+    np.testing.assert_allclose(got, fx[f"rew_{variant}"], rtol=1e-6, atol=1e-5)
+    gpu.close()
+
+
+def test_gpu_terminal_override(ms):
+    n = 4
+    gpu = ms.SoccerBatch(n, config=cfg_dict(score_difference_multiplier=5.0))
+    pos = np.random.default_rng(0).uniform(20, 500, (n, 5, 2)).astype(np.float32)
+    score = np.array([[0, 0], [2, 1], [0, 3], [4, 4]], np.int32)
+    got = gpu.debug_rewards(pos, pos, np.array([0, 1, 2, 0], np.int8), np.ones(n, np.uint8), score).cpu().numpy()
+    np.testing.assert_array_equal(got[:, 0], 5.0 * (score[:, 0] - score[:, 1]))
+    gpu.close()
+
+
+# ---- edge cases --------------------------------------------------------------------------
+
+def test_nonfinite_actions_skip_env_and_count(ms):
+    n = 64
+    gpu = ms.SoccerBatch(n)
+    gpu.reset(seed=1)
+    before = gpu.export_state()
+    act = torch.zeros((n, 4, 3), device=gpu.device)
+    act[5, 2, 1] = float("nan")
+    act[9, 0, 0] = float("inf")
+    gpu.step(act)
+    st = gpu.export_state()
+    s = gpu.stats()
+    assert s["nonfinite_envs"] == 2 and s["first_nonfinite_env"] == 5
+    np.testing.assert_array_equal(st[[5, 9]]["body"]["px"], before[[5, 9]]["body"]["px"])
+    assert (st["steps"][[5, 9]] == 0).all() and (np.delete(st["steps"], [5, 9]) == 1).all()
+    gpu.close()
+
+
+def test_single_env_and_ragged_sizes(ms):
+    for n in (1, 63, 65, 1000):
+        c = run_pair(ms, n, 30, seed=n, chase=False, check_state_every=30)
+        assert c["dones"] == 0
+
+
+def test_actions_out_of_range_are_clipped(ms):
+    n = 32
+    gpu = ms.SoccerBatch(n)
+    ref = orc.OracleBatch(n, "f32")
+    gpu.reset(seed=2)
+    ref.reset(np.stack([orc.pcg_from_seed(2 + i) for i in range(n)]), 0)
+    for t in range(50):
+        act = (sh.hash_actions(n, t) * 7.5).astype(np.float32)
+        out = gpu.step(torch.from_numpy(act).to(gpu.device))
+        obs = ref.step(act)[0]
+        np.testing.assert_array_equal(out.obs.cpu().numpy(), obs)
+    gpu.close()
+
+
+# ---- full-size properties (BASELINE configs) ------------------------------------------------
+
+@pytest.mark.parametrize("n", [4096, 65536])
+def test_full_size_subsample_and_invariants(ms, n):
+    """Config 2/3 sizes: the 64-env subsample matches the fp32 oracle bit for bit, state stays
+    finite and inside the field, results are independent of the batch they run in."""
+    steps = 120
+    gpu = ms.SoccerBatch(n, config=cfg_dict(max_steps=50))
+    gpu.reset(seed=19)
+    sub = np.linspace(0, n - 1, 64).astype(np.int64)
+    ref = orc.OracleBatch(64, "f32", oracle_cfg(gpu._cfg))
+    ref.reset(np.stack([orc.pcg_from_seed(19 + int(i)) for i in sub]), 0)
+    for t in range(steps):
+        act = sh.hash_actions(n, t)
+        out = gpu.step(torch.from_numpy(act).to(gpu.device))
+        robs = ref.step(act[sub])[0]
+        if t % 20 == 19:
+            np.testing.assert_array_equal(out.obs.cpu().numpy()[sub], robs, err_msg=f"t={t}")
+    st = gpu.export_state()
+    assert np.isfinite(st["body"]["px"]).all() and np.isfinite(st["body"]["vx"]).all()
+    assert (st["body"]["px"] > -50).all() and (st["body"]["px"] < 850).all()
+    assert (st["body"]["py"] > -50).all() and (st["body"]["py"] < 650).all()
+    assert gpu.stats()["arbiter_overflow"] == 0
+    gpu.close()
