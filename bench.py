@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the MI355X soccer env step (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--allgather]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One "step" = one env.step of every env resident on a GPU (one ms_step launch): E envs per
+GPU (default 65,536 = BASELINE.json configs[2]), weak scaling across ranks (envs are
+independent; no collective in the data path). Actions are synthetic uniform(-1, 1) fp32
+generated on the device before the timed region and read from HBM every step. Rank 0
+prints ONE JSON line. --allgather adds the optional RCCL all-gather of obs (configs[3]).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "marl-soccer_amd"))
+
+METRIC = "env-steps/sec (4 agents × N envs) at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# Algorithmic HBM bytes per env-step of ms_step_kernel (DESIGN.md "Roofline"):
+ALG_READ = 48 + 176 + 12 + 704      # actions, bodies, scalars, 2-frame obs history
+ALG_WRITE = 176 + 12 + 352 + 1056 + 16 + 4 + 4 + 1 + 8  # bodies, scalars, new frame, obs, rew, term, trunc, goal, score
+ARB_BYTES = 20                       # one cached arbiter: header + 4 impulses (read + rewritten)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--action-sets", type=int, default=64, help="distinct device action buffers cycled")
+    ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of obs after every step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-envs", type=int, default=16384)
+    ap.add_argument("--cpu-steps", type=int, default=1500)
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The oracle's f64 restatement (reference precision) on this host's cores, bounded."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    n, k = args.cpu_envs, args.cpu_steps
+    secs = orc.cpu_baseline(n, k, cores, "f64")
+    return {"value": n * k / secs, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "sample": f"oracle f64 (C restatement of Game.step + Chipmunk) {n} envs x {k} steps, "
+                      f"random actions, {cores} threads, {secs:.2f} s wall"}
+
+
+def load_pmc_traffic():
+    path = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from marlsoccer import SoccerBatch
+
+    E = args.envs
+    batch = SoccerBatch(E, device=dev.index)
+    batch.reset(seed=19 + rank * E)  # env i of rank r seeded 19 + r*E + i (global index)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + rank)
+    nsets = max(1, min(args.action_sets, args.steps + args.warmup))
+    actions = [torch.rand((E, 4, 3), device=dev, generator=gen) * 2 - 1 for _ in range(nsets)]
+    obs, rew = batch.obs, batch.rew
+    term, trunc, goal, score = batch.term, batch.trunc, batch.goal, batch.score
+    gathered = None
+    if args.allgather and world > 1:
+        gathered = torch.empty((world * E, 4, 66), dtype=torch.float32, device=dev)
+
+    launch = batch.launcher(actions, obs, rew, term, trunc, goal, score)
+
+    def one(i):
+        launch(i)
+        if gathered is not None:
+            dist.all_gather_into_tensor(gathered, obs)
+
+    for i in range(args.warmup):
+        one(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        launch(args.warmup + i)
+        ev[i][1].record(stream)
+        if gathered is not None:
+            dist.all_gather_into_tensor(gathered, obs)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    st = batch.export_state()
+    mean_arb = float(st["n_arb"].mean())
+    stats = batch.stats()
+    bytes_per_step = ALG_READ + ALG_WRITE + 2 * ARB_BYTES * mean_arb
+    achieved = bytes_per_step * E / (kern_ms * 1e-3) / 1e9
+    value = world * E * args.steps / elapsed
+    if rank == 0:
+        pmc = load_pmc_traffic()
+        traffic = None
+        pmc_info = None
+        if pmc and pmc.get("envs") == E:
+            # HBM bytes per launch from the committed rocprofv3 PMC passes, over the live kernel time
+            traffic = pmc["hbm_bytes_per_launch"] / (kern_ms * 1e-3) / 1e9
+            pmc_info = {"source": f"profiles/{pmc['tag']}_pmc.json", "bytes_per_launch": pmc["hbm_bytes_per_launch"],
+                        "alg_bytes_per_launch": bytes_per_step * E}
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: uniform(-1,1) fp32 actions (device Philox, read from HBM each step); "
+                    "env i seeded 19+i; default config.json physics/rewards",
+            "config": {"workload": f"{E} parallel envs per MI355X (BASELINE.json configs[2])",
+                       "envs_per_gpu": E, "global_envs": world * E, "max_steps": 1000,
+                       "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else "")},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "ms_step_kernel", "kernel_ms": kern_ms,
+                         "alg_bytes_per_env_step": bytes_per_step, "mean_cached_arbiters": mean_arb,
+                         "pmc": pmc_info},
+            "arbiter_overflow": stats["arbiter_overflow"],
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline(args)
+            cb["gpu_over_cpu"] = value / cb["value"]
+            line["cpu_baseline"] = cb
+        print(json.dumps(line), flush=True)
+    batch.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

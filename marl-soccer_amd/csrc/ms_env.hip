@@ -29,7 +29,12 @@
 
 using namespace ms;
 
+#ifndef MS_BLOCK
 #define MS_BLOCK 64
+#endif
+#ifndef MS_ABLATE
+#define MS_ABLATE 0  // diagnostic builds only: 1 no solver, 2 no narrowphase, 3 no obs stores
+#endif
 #define MAXA MS_MAX_ARBITERS
 
 // ---- plane indices -----------------------------------------------------------------------
@@ -121,6 +126,23 @@ __device__ __forceinline__ void store_rng(const DevState& S, int64_t e, Env& E) 
   E.meta = (E.meta & ~META_H32) | (E.rng.has32 ? META_H32 : 0u);
 }
 
+// ---- LDS scratchpad ------------------------------------------------------------------------
+// Layouts are [field][index][lane]: the 64 lanes of a wave hit 64 distinct dwords whatever
+// body/box each lane selects, so dynamic per-lane indexing is bank-conflict free.
+enum { SV_VX = 0, SV_VY, SV_W, SV_VBX, SV_VBY, SV_WB, SV_PX, SV_PY, SV_N };
+enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
+#define OBS_LD 67  // padded obs staging row: lanes l and l+16 fall in different banks
+
+struct Lds {
+  union {
+    struct {
+      float v[SV_N][6][MS_BLOCK];    // body p, v, w, v_bias, w_bias (body 5 = static, all 0)
+      float box[BX_N][4][MS_BLOCK];  // agent box transform (p, cos, sin)
+    } ph;
+    float obs[MS_BLOCK][OBS_LD];     // one agent's 66-float obs row per env, staged for stores
+  };
+};
+
 // ---- frames -----------------------------------------------------------------------------
 __device__ __forceinline__ void frame_of(const Params& P, const Env& E, int agent, float* o) {
   switch (agent) {
@@ -131,47 +153,59 @@ __device__ __forceinline__ void frame_of(const Params& P, const Env& E, int agen
   }
 }
 
-// Write the stacked obs for one env: [t-2, t-1, t] per agent (soccer_env.py:130-140) and
-// advance the history ring. reset: all three slots are the new frame (soccer_env.py:90-96).
-__device__ __forceinline__ void emit_frames(const DevState& S, const Params& P, int64_t e, Env& E, bool fill3,
-                                            float* __restrict__ obs) {
+// Stacked obs [t-2, t-1, t] per agent (soccer_env.py:130-140) and the history ring update;
+// fill3: all three slots are the new frame (reset, soccer_env.py:90-96). Rows are staged in
+// LDS and written cooperatively by the whole wave (each store instruction covers two
+// consecutive 264-B rows instead of 64 rows 1056 B apart). Every lane of the block must call
+// this; `active` lanes contribute rows, `row_mask` selects which rows are stored.
+__device__ __forceinline__ void emit_frames(const DevState& S, const Params& P, int64_t e, Env& E, bool active,
+                                            bool fill3, float* __restrict__ obs, Lds& L, int lane,
+                                            uint64_t row_mask, int64_t e0) {
   const int64_t n = S.n;
   const int head = (E.meta & META_RING) ? 1 : 0;  // slot holding t-1; the other holds t-2
   const int old = head ^ 1;
 #pragma unroll 1
   for (int a = 0; a < 4; ++a) {
-    float f[22];
-    frame_of(P, E, a, f);
-    float* o = obs ? obs + e * 264 + a * 66 : nullptr;
-    if (fill3) {
+    if (active) {
+      float f[22];
+      frame_of(P, E, a, f);
+      float* row = L.obs[lane];
+      if (fill3) {
 #pragma unroll
-      for (int k = 0; k < 22; ++k) {
-        S.F[(int64_t)(F_HIST + 0 * 88 + a * 22 + k) * n + e] = f[k];
-        S.F[(int64_t)(F_HIST + 1 * 88 + a * 22 + k) * n + e] = f[k];
-      }
-      if (o) {
+        for (int k = 0; k < 22; ++k) {
+          S.F[(int64_t)(F_HIST + 0 * 88 + a * 22 + k) * n + e] = f[k];
+          S.F[(int64_t)(F_HIST + 1 * 88 + a * 22 + k) * n + e] = f[k];
+          row[k] = f[k]; row[22 + k] = f[k]; row[44 + k] = f[k];
+        }
+      } else {
+        float* ho = S.F + (int64_t)(F_HIST + old * 88 + a * 22) * n + e;
+        float* hn = S.F + (int64_t)(F_HIST + head * 88 + a * 22) * n + e;
+        float t2[22], t1[22];
 #pragma unroll
-        for (int s = 0; s < 3; ++s)
+        for (int k = 0; k < 22; ++k) { t2[k] = ho[k * n]; t1[k] = hn[k * n]; }
 #pragma unroll
-          for (int k = 0; k < 22; k += 2) *(float2*)(o + s * 22 + k) = make_float2(f[k], f[k + 1]);
-      }
-    } else {
-      float* ho = S.F + (int64_t)(F_HIST + old * 88 + a * 22) * n + e;
-      float* hn = S.F + (int64_t)(F_HIST + head * 88 + a * 22) * n + e;
-      if (o) {
-#pragma unroll
-        for (int k = 0; k < 22; k += 2) {
-          *(float2*)(o + k) = make_float2(ho[k * n], ho[(k + 1) * n]);
-          *(float2*)(o + 22 + k) = make_float2(hn[k * n], hn[(k + 1) * n]);
-          *(float2*)(o + 44 + k) = make_float2(f[k], f[k + 1]);
+        for (int k = 0; k < 22; ++k) {
+          row[k] = t2[k]; row[22 + k] = t1[k]; row[44 + k] = f[k];
+          ho[k * n] = f[k];  // new frame replaces t-2
         }
       }
-#pragma unroll
-      for (int k = 0; k < 22; ++k) ho[k * n] = f[k];  // new frame replaces t-2
     }
+    __syncthreads();
+    if (obs) {
+      // 64 rows x 33 float2 per agent; consecutive lanes store consecutive float2 of a row
+#pragma unroll 1
+      for (int q = lane; q < MS_BLOCK * 33; q += MS_BLOCK) {
+        const int r = q / 33, k2 = q - r * 33;
+        if ((row_mask >> r) & 1ull)
+          *(float2*)(obs + (e0 + r) * 264 + a * 66 + 2 * k2) = make_float2(L.obs[r][2 * k2], L.obs[r][2 * k2 + 1]);
+      }
+    }
+    __syncthreads();
   }
-  if (fill3) E.meta &= ~(META_HE | META_RING);
-  else E.meta ^= META_RING;
+  if (active) {
+    if (fill3) E.meta &= ~(META_HE | META_RING);
+    else E.meta ^= META_RING;
+  }
 }
 
 // Game.reset (game.py:76-118): fresh bodies, score/steps 0, arbiters dropped, spawn.
@@ -201,26 +235,243 @@ __device__ __forceinline__ void soft_reset_regs(Env& E) {
 }
 
 // ---- physics: cpSpaceStep restated ---------------------------------------------------------
-struct Contact {
-  float r1x, r1y, r2x, r2y, nMass, tMass, bias, bounce, jn, jt, jb;
-  int hash;
+// One contact of the per-step arbiter list (cpArbiter + cpContact fields the solver uses).
+struct CSlot {
+  float r1x, r1y, r2x, r2y, nx, ny, u;
+  float nMass, tMass, bias, bounce, jn, jt, jb;
+  uint32_t m;  // ba 0-2 | bb 3-5 | warm 6 | cidx 7 | count 8-9 | hash 10-17 | cache pos 18-23 | pair 24-29
 };
-struct Arb {
-  int pair, ba, bb, count, warm;
-  float nx, ny, e, u;
-  Contact c[2];
-};
+#define CS_BA(m) ((int)((m) & 7u))
+#define CS_BB(m) ((int)(((m) >> 3) & 7u))
+#define CS_WARM(m) (((m) >> 6) & 1u)
+#define CS_CIDX(m) (((m) >> 7) & 1u)
+#define CS_COUNT(m) (((m) >> 8) & 3u)
+#define CS_HASH(m) (((m) >> 10) & 0xffu)
+#define CS_POS(m) ((int)(((m) >> 18) & 63u))
+#define CS_PAIR(m) ((int)(((m) >> 24) & 63u))
 
-// LDS body velocity file used by the solver: [field][body 0..5][lane]; body 5 = static (0).
-enum { SV_VX = 0, SV_VY, SV_W, SV_VBX, SV_VBY, SV_WB, SV_PX, SV_PY, SV_N };
-
-struct Lds {
-  float v[SV_N][6][MS_BLOCK];
-};
+#define KREG 8                          // contacts held in registers
+#define MAXC (2 * MAXA)                 // contact capacity (2 per arbiter)
 
 __device__ __forceinline__ float cache_field(const DevState& S, int par, int k, int f, int64_t e) {
   return S.CJ[((int64_t)(par * MAXA + k) * 4 + f) * S.n + e];
 }
+__device__ __forceinline__ void cache_write(const DevState& S, int par, int k, int64_t e, uint32_t hdr, float j0,
+                                            float j1, float j2, float j3) {
+  S.CH[(int64_t)(par * MAXA + k) * S.n + e] = hdr;
+  S.CJ[((int64_t)(par * MAXA + k) * 4 + 0) * S.n + e] = j0;
+  S.CJ[((int64_t)(par * MAXA + k) * 4 + 1) * S.n + e] = j1;
+  S.CJ[((int64_t)(par * MAXA + k) * 4 + 2) * S.n + e] = j2;
+  S.CJ[((int64_t)(par * MAXA + k) * 4 + 3) * S.n + e] = j3;
+}
+
+// Per-lane working set of the contact pipeline.
+struct Contacts {
+  CSlot reg[KREG];
+  CSlot* ovf;  // overflow slots KREG..MAXC-1 (private memory; only pile-ups reach it)
+  int nc, na;
+};
+
+__device__ __forceinline__ void slot_put(Contacts& C, int k, const CSlot& s) {
+  if (k < KREG) {
+#pragma unroll
+    for (int q = 0; q < KREG; ++q)
+      if (q == k) C.reg[q] = s;
+  } else {
+    C.ovf[k - KREG] = s;
+  }
+}
+
+// cpArbiterPreStep for one contact (velocities: previous step's post-solve values)
+__device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds& L, int lane) {
+  const int ba = CS_BA(c.m), bb = CS_BB(c.m);
+  const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
+  const int p = CS_PAIR(c.m);
+  const float e = p < 6 ? P.e_aa : (p < 10 ? P.e_ab : (p < 42 ? (((p - 10) & 7) < 6 ? P.e_aw : P.e_ag) : P.e_bw));
+  const V2 n = v2(c.nx, c.ny);
+  const V2 body_delta = v2(L.ph.v[SV_PX][bb][lane] - L.ph.v[SV_PX][ba][lane], L.ph.v[SV_PY][bb][lane] - L.ph.v[SV_PY][ba][lane]);
+  const V2 va = v2(L.ph.v[SV_VX][ba][lane], L.ph.v[SV_VY][ba][lane]);
+  const V2 vb = v2(L.ph.v[SV_VX][bb][lane], L.ph.v[SV_VY][bb][lane]);
+  const float wa = L.ph.v[SV_W][ba][lane], wbv = L.ph.v[SV_W][bb][lane];
+  const V2 r1 = v2(c.r1x, c.r1y), r2 = v2(c.r2x, c.r2y);
+  const float rcn1 = vcross(r1, n), rcn2 = vcross(r2, n);
+  c.nMass = 1.0f / ((ma + ia * rcn1 * rcn1) + (mb + ib * rcn2 * rcn2));
+  const V2 t = vperp(n);
+  const float rct1 = vcross(r1, t), rct2 = vcross(r2, t);
+  c.tMass = 1.0f / ((ma + ia * rct1 * rct1) + (mb + ib * rct2 * rct2));
+  const float dist = vdot(vadd(vsub(r2, r1), body_delta), n);
+  c.bias = -P.bias_coef * fminr(0.0f, dist + P.slop) / P.dt;
+  c.jb = 0.0f;
+  const V2 v1 = vadd(va, vmult(vperp(r1), wa));
+  const V2 v2s = vadd(vb, vmult(vperp(r2), wbv));
+  c.bounce = vdot(vsub(v2s, v1), n) * e;
+}
+
+// cpArbiterApplyCachedImpulse for one contact (dt_coef = 1)
+__device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L, int lane) {
+  if (!CS_WARM(c.m)) return;
+  const int ba = CS_BA(c.m), bb = CS_BB(c.m);
+  const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
+  const V2 j = vrotate(v2(c.nx, c.ny), v2(c.jn, c.jt));
+  const V2 nj = vneg(j);
+  L.ph.v[SV_VX][ba][lane] = L.ph.v[SV_VX][ba][lane] + nj.x * ma;
+  L.ph.v[SV_VY][ba][lane] = L.ph.v[SV_VY][ba][lane] + nj.y * ma;
+  L.ph.v[SV_W][ba][lane] += ia * vcross(v2(c.r1x, c.r1y), nj);
+  L.ph.v[SV_VX][bb][lane] = L.ph.v[SV_VX][bb][lane] + j.x * mb;
+  L.ph.v[SV_VY][bb][lane] = L.ph.v[SV_VY][bb][lane] + j.y * mb;
+  L.ph.v[SV_W][bb][lane] += ib * vcross(v2(c.r2x, c.r2y), j);
+}
+
+// cpArbiterApplyImpulse for one contact
+__device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int lane) {
+  const int ba = CS_BA(c.m), bb = CS_BB(c.m);
+  const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
+  const V2 n = v2(c.nx, c.ny);
+  const V2 r1 = v2(c.r1x, c.r1y), r2 = v2(c.r2x, c.r2y);
+  const float vbxa = L.ph.v[SV_VBX][ba][lane], vbya = L.ph.v[SV_VBY][ba][lane], wba = L.ph.v[SV_WB][ba][lane];
+  const float vbxb = L.ph.v[SV_VBX][bb][lane], vbyb = L.ph.v[SV_VBY][bb][lane], wbb = L.ph.v[SV_WB][bb][lane];
+  const float vxa = L.ph.v[SV_VX][ba][lane], vya = L.ph.v[SV_VY][ba][lane], wa = L.ph.v[SV_W][ba][lane];
+  const float vxb = L.ph.v[SV_VX][bb][lane], vyb = L.ph.v[SV_VY][bb][lane], wb_ = L.ph.v[SV_W][bb][lane];
+  const V2 vb1 = vadd(v2(vbxa, vbya), vmult(vperp(r1), wba));
+  const V2 vb2 = vadd(v2(vbxb, vbyb), vmult(vperp(r2), wbb));
+  const V2 vs1 = vadd(v2(vxa, vya), vmult(vperp(r1), wa));
+  const V2 vs2 = vadd(v2(vxb, vyb), vmult(vperp(r2), wb_));
+  const V2 vr = vsub(vs2, vs1);
+  const float vbn = vdot(vsub(vb2, vb1), n);
+  const float vrn = vdot(vr, n);
+  const float vrt = vdot(vr, vperp(n));
+
+  const float jbn = (c.bias - vbn) * c.nMass;
+  const float jbnOld = c.jb;
+  c.jb = fmaxr(jbnOld + jbn, 0.0f);
+
+  const float jn = -(c.bounce + vrn) * c.nMass;
+  const float jnOld = c.jn;
+  c.jn = fmaxr(jnOld + jn, 0.0f);
+
+  const float jtMax = c.u * c.jn;
+  const float jt = -vrt * c.tMass;
+  const float jtOld = c.jt;
+  c.jt = fclamp(jtOld + jt, -jtMax, jtMax);
+
+  const V2 jbv = vmult(n, c.jb - jbnOld);
+  const V2 njb = vneg(jbv);
+  const V2 j = vrotate(n, v2(c.jn - jnOld, c.jt - jtOld));
+  const V2 nj = vneg(j);
+  // body a first, then body b (apply_bias_impulses then apply_impulses, cpArbiter.c);
+  // a and b are distinct bodies, so the four updates commute per body.
+  L.ph.v[SV_VBX][ba][lane] = vbxa + njb.x * ma;
+  L.ph.v[SV_VBY][ba][lane] = vbya + njb.y * ma;
+  L.ph.v[SV_WB][ba][lane] = wba + ia * vcross(r1, njb);
+  L.ph.v[SV_VBX][bb][lane] = vbxb + jbv.x * mb;
+  L.ph.v[SV_VBY][bb][lane] = vbyb + jbv.y * mb;
+  L.ph.v[SV_WB][bb][lane] = wbb + ib * vcross(r2, jbv);
+  L.ph.v[SV_VX][ba][lane] = vxa + nj.x * ma;
+  L.ph.v[SV_VY][ba][lane] = vya + nj.y * ma;
+  L.ph.v[SV_W][ba][lane] = wa + ia * vcross(r1, nj);
+  L.ph.v[SV_VX][bb][lane] = vxb + j.x * mb;
+  L.ph.v[SV_VY][bb][lane] = vyb + j.y * mb;
+  L.ph.v[SV_W][bb][lane] = wb_ + ib * vcross(r2, j);
+}
+
+__device__ __forceinline__ void lds_box(const Lds& L, int i, int lane, Box& b) {
+  box_world(L.ph.box[BX_PX][i][lane], L.ph.box[BX_PY][i][lane], L.ph.box[BX_C][i][lane], L.ph.box[BX_S][i][lane], b);
+}
+
+// Old-cache cursor: the previous step's arbiter cache (sorted by pair id) is streamed once,
+// merged with this step's touched arbiters into the other (ping-pong) buffer.
+struct CacheWalk {
+  int par, nc_old, cur, out;
+  uint32_t curh;
+};
+
+__device__ __forceinline__ void cache_advance(const DevState& S, int64_t e, CacheWalk& W) {
+  ++W.cur;
+  W.curh = W.cur < W.nc_old ? S.CH[(int64_t)(W.par * MAXA + W.cur) * S.n + e] : 0xffffffffu;
+}
+
+// emit the old entry under the cursor aged by one step (dropped at idle 3, cpSpaceArbiterSetFilter)
+__device__ __forceinline__ void cache_age_current(const DevState& S, int64_t e, CacheWalk& W,
+                                                  unsigned long long* overflow_acc) {
+  const uint32_t idle = ((W.curh >> 8) & 3u) + 1u;
+  if (idle < 3u) {
+    if (W.out < MAXA) {
+      cache_write(S, W.par ^ 1, W.out, e, (W.curh & ~(3u << 8)) | (idle << 8), cache_field(S, W.par, W.cur, 0, e),
+                  cache_field(S, W.par, W.cur, 1, e), cache_field(S, W.par, W.cur, 2, e),
+                  cache_field(S, W.par, W.cur, 3, e));
+      ++W.out;
+    } else {
+      (*overflow_acc)++;
+    }
+  }
+  cache_advance(S, e, W);
+}
+
+// cpSpaceCollideShapes + cpArbiterUpdate for one touching pair
+__device__ __forceinline__ void add_arbiter(const DevState& S, int64_t e, const Lds& L, int lane, Contacts& C,
+                                            CacheWalk& W, int p, int ba, int bb, const Col& col, float u,
+                                            unsigned long long* overflow_acc) {
+  if (C.na >= MAXA) { (*overflow_acc)++; return; }
+  while (W.cur < W.nc_old && (int)(W.curh & 63u) < p) cache_age_current(S, e, W, overflow_acc);
+  const bool found = W.cur < W.nc_old && (int)(W.curh & 63u) == p;
+  const uint32_t oh = W.curh;
+  float oj[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (found) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) oj[f] = cache_field(S, W.par, W.cur, f, e);
+    cache_advance(S, e, W);
+  }
+  int pos = W.out;
+  if (W.out < MAXA) ++W.out; else { (*overflow_acc)++; pos = 63; }
+  C.na++;
+  const float ax = L.ph.v[SV_PX][ba][lane], ay = L.ph.v[SV_PY][ba][lane];
+  const float bx = L.ph.v[SV_PX][bb][lane], by = L.ph.v[SV_PY][bb][lane];
+  const uint32_t warm = (found && ((oh >> 8) & 3u) == 0u) ? 1u : 0u;
+  for (int k = 0; k < col.count; ++k) {
+    CSlot s;
+    const V2 p1 = k == 0 ? col.p1[0] : col.p1[1];
+    const V2 p2 = k == 0 ? col.p2[0] : col.p2[1];
+    const int h = k == 0 ? col.hash[0] : col.hash[1];
+    s.r1x = p1.x - ax; s.r1y = p1.y - ay;
+    s.r2x = p2.x - bx; s.r2y = p2.y - by;
+    s.nx = col.n.x; s.ny = col.n.y; s.u = u;
+    s.nMass = 0.0f; s.tMass = 0.0f; s.bias = 0.0f; s.bounce = 0.0f; s.jb = 0.0f;
+    s.jn = 0.0f; s.jt = 0.0f;
+    if (found) {
+      const int ocount = (oh >> 6) & 3u;
+      for (int j = 0; j < ocount; ++j)
+        if ((int)((oh >> (16 + 8 * j)) & 0xffu) == h) { s.jn = oj[2 * j]; s.jt = oj[2 * j + 1]; }
+    }
+    s.m = (uint32_t)ba | ((uint32_t)bb << 3) | (warm << 6) | ((uint32_t)k << 7) | ((uint32_t)col.count << 8) |
+          ((uint32_t)(h & 0xff) << 10) | ((uint32_t)pos << 18) | ((uint32_t)p << 24);
+    slot_put(C, C.nc, s);
+    C.nc++;
+  }
+}
+
+// cache entry of a touched arbiter from its first contact c0 (and c1 when it has two)
+__device__ __forceinline__ void write_arbiter_cache(const DevState& S, int npar, int64_t e, const CSlot& c0,
+                                                    const CSlot& c1) {
+  if (CS_CIDX(c0.m) != 0 || CS_POS(c0.m) >= MAXA) return;
+  const bool two = CS_COUNT(c0.m) > 1;
+  const uint32_t hdr = (uint32_t)CS_PAIR(c0.m) | (CS_COUNT(c0.m) << 6) | (CS_HASH(c0.m) << 16) |
+                       ((two ? CS_HASH(c1.m) : 0u) << 24);
+  cache_write(S, npar, CS_POS(c0.m), e, hdr, c0.jn, c0.jt, two ? c1.jn : 0.0f, two ? c1.jt : 0.0f);
+}
+
+#define FOR_CONTACTS(C, BODY)                                         \
+  {                                                                   \
+    _Pragma("unroll") for (int k_ = 0; k_ < KREG; ++k_) {             \
+      if (k_ < (C).nc) {                                              \
+        CSlot& c_ = (C).reg[k_];                                      \
+        BODY;                                                         \
+      }                                                               \
+    }                                                                 \
+    for (int k_ = KREG; k_ < (C).nc; ++k_) {                          \
+      CSlot& c_ = (C).ovf[k_ - KREG];                                 \
+      BODY;                                                           \
+    }                                                                 \
+  }
 
 __device__ __forceinline__ void physics_step(const DevState& S, const Params& P, int64_t e, Env& E, float fx[4],
                                              float fy[4], float tq[4], Lds& L, int lane,
@@ -234,134 +485,109 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     if (b < 4) E.ang[b] = E.ang[b] + (E.w[b] + E.wb[b]) * dt;
     E.vbx[b] = 0.0f; E.vby[b] = 0.0f; E.wb[b] = 0.0f;
   }
-  Box box[4];
+  // shape caches; agents' transforms go to LDS for per-lane dynamic access
+  float bb_[4][4];
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     float s, c;
     sincos_contract(E.ang[b], &s, &c);
-    box_world(E.px[b], E.py[b], c, s, box[b]);
+    Box bx;
+    box_world(E.px[b], E.py[b], c, s, bx);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bb_[b][q] = bx.bb[q];
+    L.ph.box[BX_PX][b][lane] = E.px[b]; L.ph.box[BX_PY][b][lane] = E.py[b];
+    L.ph.box[BX_C][b][lane] = c; L.ph.box[BX_S][b][lane] = s;
   }
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    L.ph.v[SV_PX][b][lane] = E.px[b]; L.ph.v[SV_PY][b][lane] = E.py[b];
+    L.ph.v[SV_VX][b][lane] = E.vx[b]; L.ph.v[SV_VY][b][lane] = E.vy[b]; L.ph.v[SV_W][b][lane] = E.w[b];
+    L.ph.v[SV_VBX][b][lane] = 0.0f; L.ph.v[SV_VBY][b][lane] = 0.0f; L.ph.v[SV_WB][b][lane] = 0.0f;
+  }
+#pragma unroll
+  for (int f = 0; f < SV_N; ++f) L.ph.v[f][5][lane] = 0.0f;
   const V2 ballc = v2(E.px[4], E.py[4]);
   const float BR = 10.0f;
   const float ballbb[4] = {ballc.x - BR, ballc.y - BR, ballc.x + BR, ballc.y + BR};
 
-  const int par = (E.meta & META_PAR) ? 1 : 0;
-  const int nc = META_NC(E.meta);
-  Arb arb[MAXA];
-  int na = 0;
-  int cur = 0;  // merge cursor into the (pair-sorted) old cache
-  uint32_t curh = nc > 0 ? S.CH[(int64_t)(par * MAXA + 0) * S.n + e] : 0xffffffffu;
-
-  // narrowphase per shape pair in canonical order (cpSpaceCollideShapes + cpArbiterUpdate)
-  auto add_arbiter = [&](int p, int ba, int bb, const Col& col, float ee, float uu) {
-    if (na >= MAXA) { (*overflow_acc)++; return; }
-    while (cur < nc && (int)(curh & 63u) < p) {
-      ++cur;
-      curh = cur < nc ? S.CH[(int64_t)(par * MAXA + cur) * S.n + e] : 0xffffffffu;
-    }
-    const bool found = cur < nc && (int)(curh & 63u) == p;
-    Arb& A = arb[na++];
-    A.pair = p; A.ba = ba; A.bb = bb; A.count = col.count;
-    A.warm = found && ((curh >> 8) & 3u) == 0u;
-    A.nx = col.n.x; A.ny = col.n.y; A.e = ee; A.u = uu;
-    for (int k = 0; k < col.count; ++k) {
-      Contact& C = A.c[k];
-      float ax = 0.0f, ay = 0.0f, bx = 0.0f, by = 0.0f;
+  // broadphase: AABB masks per pair class (cpBBIntersects), no divergence
+  uint32_t mAA = 0, mBA = 0, mSA = 0, mBS = 0;
+  {
+    const int AI[6] = {0, 0, 0, 1, 1, 2}, AJ[6] = {1, 2, 3, 2, 3, 3};
 #pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        if (q == ba) { ax = E.px[q]; ay = E.py[q]; }
-        if (q == bb) { bx = E.px[q]; by = E.py[q]; }
-      }
-      C.r1x = col.p1[k].x - ax; C.r1y = col.p1[k].y - ay;
-      C.r2x = col.p2[k].x - bx; C.r2y = col.p2[k].y - by;
-      C.hash = col.hash[k];
-      C.jn = 0.0f; C.jt = 0.0f;
-      if (found) {
-        const int ocount = (curh >> 6) & 3u;
-        for (int j = 0; j < ocount; ++j) {
-          const int oh = (curh >> (16 + 8 * j)) & 0xffu;
-          if (oh == C.hash) {
-            C.jn = cache_field(S, par, cur, 2 * j, e);
-            C.jt = cache_field(S, par, cur, 2 * j + 1, e);
-          }
-        }
-      }
-    }
-  };
-
-  // agent-agent (pairs 0-5)
+    for (int p = 0; p < 6; ++p)
+      if (bb_intersects(bb_[AI[p]], bb_[AJ[p]])) mAA |= 1u << p;
 #pragma unroll
-  for (int p = 0; p < 6; ++p) {
+    for (int i = 0; i < 4; ++i) {
+      if (bb_intersects(ballbb, bb_[i])) mBA |= 1u << i;
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        if (bb_intersects(P.seg[s].bb, bb_[i])) mSA |= 1u << (i * 8 + s);
+    }
+#pragma unroll
+    for (int s = 0; s < 6; ++s)
+      if (bb_intersects(ballbb, P.seg[s].bb)) mBS |= 1u << s;
+  }
+#if MS_ABLATE == 2
+  mAA = mBA = mSA = mBS = 0;
+#endif
+
+  CSlot ovf_store[MAXC - KREG];
+  Contacts C;
+  C.ovf = ovf_store;
+  C.nc = 0;
+  C.na = 0;
+  CacheWalk W;
+  W.par = (E.meta & META_PAR) ? 1 : 0;
+  W.nc_old = META_NC(E.meta);
+  W.cur = 0;
+  W.out = 0;
+  W.curh = W.nc_old > 0 ? S.CH[(int64_t)(W.par * MAXA + 0) * S.n + e] : 0xffffffffu;
+
+  // narrowphase, one compacted loop per pair class so each lane visits only its own touching
+  // pairs; class order + ctz order = canonical pair order (DESIGN.md pair table)
+  while (mAA) {
+    const int p = __builtin_ctz(mAA);
+    mAA &= mAA - 1;
     const int i = p < 3 ? 0 : (p < 5 ? 1 : 2);
-    const int j = p == 0 ? 1 : (p == 1 ? 2 : (p == 2 ? 3 : (p == 3 ? 2 : 3)));
-    if (!bb_intersects(box[i].bb, box[j].bb)) continue;
+    const int j = p < 3 ? p + 1 : (p < 5 ? p - 1 : 3);
+    Box A, B;
+    lds_box(L, i, lane, A);
+    lds_box(L, j, lane, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
-    col_box_box(box[i], box[j], col);
-    if (col.count) add_arbiter(p, i, j, col, P.e_aa, P.u_aa);
+    col_box_box(A, B, col);
+    if (col.count) add_arbiter(S, e, L, lane, C, W, p, i, j, col, P.u_aa, overflow_acc);
   }
-  // ball-agent (6-9)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (!bb_intersects(ballbb, box[i].bb)) continue;
+  while (mBA) {
+    const int i = __builtin_ctz(mBA);
+    mBA &= mBA - 1;
+    Box B;
+    lds_box(L, i, lane, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
-    col_circle_box(ballc, BR, box[i], col);
-    if (col.count) add_arbiter(6 + i, 4, i, col, P.e_ab, P.u_ab);
+    col_circle_box(ballc, BR, B, col);
+    if (col.count) add_arbiter(S, e, L, lane, C, W, 6 + i, 4, i, col, P.u_ab, overflow_acc);
   }
-  // static-agent (10-41)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll 1
-    for (int s = 0; s < 8; ++s) {
-      if (!bb_intersects(P.seg[s].bb, box[i].bb)) continue;
-      Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
-      col_seg_box(P.seg[s], box[i], col);
-      if (col.count) add_arbiter(10 + i * 8 + s, 5, i, col, s < 6 ? P.e_aw : P.e_ag, s < 6 ? P.u_aw : P.u_ag);
-    }
+  while (mSA) {
+    const int q = __builtin_ctz(mSA);
+    mSA &= mSA - 1;
+    const int i = q >> 3, s = q & 7;
+    Box B;
+    lds_box(L, i, lane, B);
+    Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
+    col_seg_box(P.seg[s], B, col);
+    if (col.count) add_arbiter(S, e, L, lane, C, W, 10 + q, 5, i, col, s < 6 ? P.u_aw : P.u_ag, overflow_acc);
   }
-  // ball-wall (42-47)
-#pragma unroll 1
-  for (int s = 0; s < 6; ++s) {
-    if (!bb_intersects(ballbb, P.seg[s].bb)) continue;
+  while (mBS) {
+    const int s = __builtin_ctz(mBS);
+    mBS &= mBS - 1;
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     col_circle_seg(ballc, BR, P.seg[s], col);
-    if (col.count) add_arbiter(42 + s, 4, 5, col, P.e_bw, P.u_bw);
+    if (col.count) add_arbiter(S, e, L, lane, C, W, 42 + s, 4, 5, col, P.u_bw, overflow_acc);
   }
+  while (W.cur < W.nc_old) cache_age_current(S, e, W, overflow_acc);
 
-  // stage positions + velocities in LDS for dynamic body indexing
-#pragma unroll
-  for (int b = 0; b < 5; ++b) {
-    L.v[SV_VX][b][lane] = E.vx[b]; L.v[SV_VY][b][lane] = E.vy[b]; L.v[SV_W][b][lane] = E.w[b];
-    L.v[SV_VBX][b][lane] = 0.0f; L.v[SV_VBY][b][lane] = 0.0f; L.v[SV_WB][b][lane] = 0.0f;
-    L.v[SV_PX][b][lane] = E.px[b]; L.v[SV_PY][b][lane] = E.py[b];
-  }
-#pragma unroll
-  for (int f = 0; f < SV_N; ++f) L.v[f][5][lane] = 0.0f;
-
-  // cpArbiterPreStep (pre-integration velocities)
-  for (int k = 0; k < na; ++k) {
-    Arb& A = arb[k];
-    const int ba = A.ba, bb = A.bb;
-    const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
-    const V2 n = v2(A.nx, A.ny);
-    const V2 body_delta = v2(L.v[SV_PX][bb][lane] - L.v[SV_PX][ba][lane], L.v[SV_PY][bb][lane] - L.v[SV_PY][ba][lane]);
-    const V2 va = v2(L.v[SV_VX][ba][lane], L.v[SV_VY][ba][lane]), vb = v2(L.v[SV_VX][bb][lane], L.v[SV_VY][bb][lane]);
-    const float wa = L.v[SV_W][ba][lane], wbv = L.v[SV_W][bb][lane];
-    for (int i = 0; i < A.count; ++i) {
-      Contact& C = A.c[i];
-      const V2 r1 = v2(C.r1x, C.r1y), r2 = v2(C.r2x, C.r2y);
-      float rcn1 = vcross(r1, n), rcn2 = vcross(r2, n);
-      C.nMass = 1.0f / ((ma + ia * rcn1 * rcn1) + (mb + ib * rcn2 * rcn2));
-      const V2 t = vperp(n);
-      float rct1 = vcross(r1, t), rct2 = vcross(r2, t);
-      C.tMass = 1.0f / ((ma + ia * rct1 * rct1) + (mb + ib * rct2 * rct2));
-      float dist = vdot(vadd(vsub(r2, r1), body_delta), n);
-      C.bias = -P.bias_coef * fminr(0.0f, dist + P.slop) / dt;
-      C.jb = 0.0f;
-      const V2 v1 = vadd(va, vmult(vperp(r1), wa));
-      const V2 v2s = vadd(vb, vmult(vperp(r2), wbv));
-      C.bounce = vdot(vsub(v2s, v1), n) * A.e;
-    }
-  }
+  // cpArbiterPreStep
+  FOR_CONTACTS(C, prestep_one(P, c_, L, lane));
 
   // cpBodyUpdateVelocity + entities.py velocity_func (damping, max-velocity clamp)
 #pragma unroll
@@ -380,131 +606,33 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
       nvx = (nvx / len) * P.vmax;
       nvy = (nvy / len) * P.vmax;
     }
-    L.v[SV_VX][b][lane] = nvx; L.v[SV_VY][b][lane] = nvy; L.v[SV_W][b][lane] = nw;
+    E.vx[b] = nvx; E.vy[b] = nvy; E.w[b] = nw;
+    L.ph.v[SV_VX][b][lane] = nvx; L.ph.v[SV_VY][b][lane] = nvy; L.ph.v[SV_W][b][lane] = nw;
   }
 
-  // cpArbiterApplyCachedImpulse
-  for (int k = 0; k < na; ++k) {
-    const Arb& A = arb[k];
-    if (!A.warm) continue;
-    const int ba = A.ba, bb = A.bb;
-    const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
-    const V2 n = v2(A.nx, A.ny);
-    for (int i = 0; i < A.count; ++i) {
-      const Contact& C = A.c[i];
-      const V2 j = vrotate(n, v2(C.jn, C.jt));
-      const V2 r1 = v2(C.r1x, C.r1y), r2 = v2(C.r2x, C.r2y);
-      const V2 nj = vneg(j);
-      L.v[SV_VX][ba][lane] = L.v[SV_VX][ba][lane] + nj.x * ma;
-      L.v[SV_VY][ba][lane] = L.v[SV_VY][ba][lane] + nj.y * ma;
-      L.v[SV_W][ba][lane] += ia * vcross(r1, nj);
-      L.v[SV_VX][bb][lane] = L.v[SV_VX][bb][lane] + j.x * mb;
-      L.v[SV_VY][bb][lane] = L.v[SV_VY][bb][lane] + j.y * mb;
-      L.v[SV_W][bb][lane] += ib * vcross(r2, j);
-    }
-  }
-
-  // cpArbiterApplyImpulse x 10
+  if (C.nc > 0) {
+    // cpArbiterApplyCachedImpulse, then cpArbiterApplyImpulse x 10 (pymunk Space default)
+    FOR_CONTACTS(C, warm_one(P, c_, L, lane));
 #pragma unroll 1
-  for (int it = 0; it < 10; ++it) {
-    for (int k = 0; k < na; ++k) {
-      Arb& A = arb[k];
-      const int ba = A.ba, bb = A.bb;
-      const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
-      const V2 n = v2(A.nx, A.ny);
-      const float friction = A.u;
-      for (int i = 0; i < A.count; ++i) {
-        Contact& C = A.c[i];
-        const float nMass = C.nMass;
-        const V2 r1 = v2(C.r1x, C.r1y), r2 = v2(C.r2x, C.r2y);
-        const V2 vb1 = vadd(v2(L.v[SV_VBX][ba][lane], L.v[SV_VBY][ba][lane]), vmult(vperp(r1), L.v[SV_WB][ba][lane]));
-        const V2 vb2 = vadd(v2(L.v[SV_VBX][bb][lane], L.v[SV_VBY][bb][lane]), vmult(vperp(r2), L.v[SV_WB][bb][lane]));
-        const V2 vs1 = vadd(v2(L.v[SV_VX][ba][lane], L.v[SV_VY][ba][lane]), vmult(vperp(r1), L.v[SV_W][ba][lane]));
-        const V2 vs2 = vadd(v2(L.v[SV_VX][bb][lane], L.v[SV_VY][bb][lane]), vmult(vperp(r2), L.v[SV_W][bb][lane]));
-        const V2 vr = vsub(vs2, vs1);
-        const float vbn = vdot(vsub(vb2, vb1), n);
-        const float vrn = vdot(vr, n);
-        const float vrt = vdot(vr, vperp(n));
-
-        const float jbn = (C.bias - vbn) * nMass;
-        const float jbnOld = C.jb;
-        C.jb = fmaxr(jbnOld + jbn, 0.0f);
-
-        const float jn = -(C.bounce + vrn) * nMass;
-        const float jnOld = C.jn;
-        C.jn = fmaxr(jnOld + jn, 0.0f);
-
-        const float jtMax = friction * C.jn;
-        const float jt = -vrt * C.tMass;
-        const float jtOld = C.jt;
-        C.jt = fclamp(jtOld + jt, -jtMax, jtMax);
-
-        const V2 jbv = vmult(n, C.jb - jbnOld);
-        const V2 njb = vneg(jbv);
-        L.v[SV_VBX][ba][lane] = L.v[SV_VBX][ba][lane] + njb.x * ma;
-        L.v[SV_VBY][ba][lane] = L.v[SV_VBY][ba][lane] + njb.y * ma;
-        L.v[SV_WB][ba][lane] += ia * vcross(r1, njb);
-        L.v[SV_VBX][bb][lane] = L.v[SV_VBX][bb][lane] + jbv.x * mb;
-        L.v[SV_VBY][bb][lane] = L.v[SV_VBY][bb][lane] + jbv.y * mb;
-        L.v[SV_WB][bb][lane] += ib * vcross(r2, jbv);
-
-        const V2 j = vrotate(n, v2(C.jn - jnOld, C.jt - jtOld));
-        const V2 nj = vneg(j);
-        L.v[SV_VX][ba][lane] = L.v[SV_VX][ba][lane] + nj.x * ma;
-        L.v[SV_VY][ba][lane] = L.v[SV_VY][ba][lane] + nj.y * ma;
-        L.v[SV_W][ba][lane] += ia * vcross(r1, nj);
-        L.v[SV_VX][bb][lane] = L.v[SV_VX][bb][lane] + j.x * mb;
-        L.v[SV_VY][bb][lane] = L.v[SV_VY][bb][lane] + j.y * mb;
-        L.v[SV_W][bb][lane] += ib * vcross(r2, j);
+    for (int it = 0; it < 10 * (MS_ABLATE != 1); ++it) FOR_CONTACTS(C, solve_one(P, c_, L, lane));
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      E.vx[b] = L.ph.v[SV_VX][b][lane]; E.vy[b] = L.ph.v[SV_VY][b][lane]; E.w[b] = L.ph.v[SV_W][b][lane];
+      E.vbx[b] = L.ph.v[SV_VBX][b][lane]; E.vby[b] = L.ph.v[SV_VBY][b][lane]; E.wb[b] = L.ph.v[SV_WB][b][lane];
+    }
+    // touched arbiters' cache entries at the positions reserved in merge order
+#pragma unroll
+    for (int k = 0; k < KREG; ++k) {
+      if (k < C.nc) {
+        const CSlot& c0 = C.reg[k];
+        const CSlot& c1 = k + 1 < KREG ? C.reg[k + 1 < KREG ? k + 1 : 0] : C.ovf[0];
+        write_arbiter_cache(S, W.par ^ 1, e, c0, c1);
       }
     }
+    for (int k = KREG; k < C.nc; ++k) write_arbiter_cache(S, W.par ^ 1, e, C.ovf[k - KREG], C.ovf[k + 1 - KREG]);
   }
-
-#pragma unroll
-  for (int b = 0; b < 5; ++b) {
-    E.vx[b] = L.v[SV_VX][b][lane]; E.vy[b] = L.v[SV_VY][b][lane]; E.w[b] = L.v[SV_W][b][lane];
-    E.vbx[b] = L.v[SV_VBX][b][lane]; E.vby[b] = L.v[SV_VBY][b][lane]; E.wb[b] = L.v[SV_WB][b][lane];
-  }
-
-  // cpSpaceArbiterSetFilter: merge touched arbiters (idle 0) with aged old entries into the
-  // other cache buffer; entries idle for 3 steps are dropped.
-  const int npar = par ^ 1;
-  int nn = 0, ia = 0, ic = 0;
-  uint32_t ch = nc > 0 ? S.CH[(int64_t)(par * MAXA + 0) * S.n + e] : 0xffffffffu;
-  while (ia < na || ic < nc) {
-    const int pa = ia < na ? arb[ia].pair : (1 << 30);
-    const int pc = ic < nc ? (int)(ch & 63u) : (1 << 30);
-    uint32_t hdr;
-    float j4[4];
-    if (pa <= pc) {
-      const Arb& A = arb[ia];
-      hdr = (uint32_t)A.pair | ((uint32_t)A.count << 6);
-      hdr |= (uint32_t)(A.c[0].hash & 0xff) << 16;
-      if (A.count > 1) hdr |= (uint32_t)(A.c[1].hash & 0xff) << 24;
-      j4[0] = A.c[0].jn; j4[1] = A.c[0].jt;
-      j4[2] = A.count > 1 ? A.c[1].jn : 0.0f;
-      j4[3] = A.count > 1 ? A.c[1].jt : 0.0f;
-      ++ia;
-      if (pa == pc) {
-        ++ic;
-        ch = ic < nc ? S.CH[(int64_t)(par * MAXA + ic) * S.n + e] : 0xffffffffu;
-      }
-    } else {
-      const uint32_t idle = ((ch >> 8) & 3u) + 1u;
-      hdr = (ch & ~(3u << 8)) | (idle << 8);
-#pragma unroll
-      for (int f = 0; f < 4; ++f) j4[f] = cache_field(S, par, ic, f, e);
-      ++ic;
-      ch = ic < nc ? S.CH[(int64_t)(par * MAXA + ic) * S.n + e] : 0xffffffffu;
-      if (idle >= 3u) continue;
-    }
-    if (nn >= MAXA) { (*overflow_acc)++; continue; }
-    S.CH[(int64_t)(npar * MAXA + nn) * S.n + e] = hdr;
-#pragma unroll
-    for (int f = 0; f < 4; ++f) S.CJ[((int64_t)(npar * MAXA + nn) * 4 + f) * S.n + e] = j4[f];
-    ++nn;
-  }
-  E.meta = (E.meta & ~((63u << 8) | META_PAR)) | ((uint32_t)nn << 8) | (npar ? META_PAR : 0u);
+  const int nn = W.out < MAXA ? W.out : MAXA;
+  E.meta = (E.meta & ~((63u << 8) | META_PAR)) | ((uint32_t)nn << 8) | (W.par ? 0u : META_PAR);
 }
 
 // ---- kernels ---------------------------------------------------------------------------------
@@ -530,109 +658,127 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
                                                            Counters* ctr) {
   __shared__ Lds L;
   const int lane = threadIdx.x;
-  const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + lane;
-  if (e >= S.n) return;
+  const int64_t e0 = (int64_t)blockIdx.x * MS_BLOCK;
+  const int64_t e = e0 + lane;
+  bool active = e < S.n;
 
   // SoccerEnv.step validation + clip + fp32 scaling (soccer_env.py:101-125)
   float a[12];
-  const float4* ap = (const float4*)(actions + e * 12);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    float4 v = ap[q];
-    a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-  }
-  bool finite = true;
+  for (int k = 0; k < 12; ++k) a[k] = 0.0f;
+  if (active) {
+    const float4* ap = (const float4*)(actions + e * 12);
 #pragma unroll
-  for (int k = 0; k < 12; ++k) finite = finite && isfinite(a[k]);
-  if (!finite) {
-    atomicAdd(&ctr->nonfinite, 1ULL);
-    atomicMin(&ctr->first_bad, (long long)e);
-    return;
-  }
-  float fx[4], fy[4], tq[4];
-  Env E;
-  load_scalars(S, e, E);
-  load_bodies(S, e, E);
-  float pvx[5], pvy[5];
-#pragma unroll
-  for (int b = 0; b < 5; ++b) { pvx[b] = E.px[b]; pvy[b] = E.py[b]; }
-  E.steps += 1;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float F[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      float v = a[i * 3 + k];
-      v = v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v);
-      F[k] = v * (k < 2 ? P.force_max : P.torque_max);
+    for (int q = 0; q < 3; ++q) {
+      float4 v = ap[q];
+      a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
     }
-    float s, c;
-    sincos_contract(E.ang[i], &s, &c);
-    fx[i] = 0.0f + (c * F[0] + (-s) * F[1]);
-    fy[i] = 0.0f + (s * F[0] + c * F[1]);
-    tq[i] = F[2];
+    bool finite = true;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) finite = finite && isfinite(a[k]);
+    if (!finite) {
+      atomicAdd(&ctr->nonfinite, 1ULL);
+      atomicMin(&ctr->first_bad, (long long)e);
+      active = false;
+    }
   }
-  unsigned long long ovf = 0;
-  physics_step(S, P, e, E, fx, fy, tq, L, lane, &ovf);
-  if (ovf) atomicAdd(&ctr->overflow, ovf);
+  const uint64_t row_mask = __ballot(active);
+  Env E;
+  float pvx[5], pvy[5];
+  bool fill3 = false, rng_dirty = false;
+  if (active) {
+    float fx[4], fy[4], tq[4];
+    load_scalars(S, e, E);
+    load_bodies(S, e, E);
+#pragma unroll
+    for (int b = 0; b < 5; ++b) { pvx[b] = E.px[b]; pvy[b] = E.py[b]; }
+    E.steps += 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float F[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        float v = a[i * 3 + k];
+        v = v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v);
+        F[k] = v * (k < 2 ? P.force_max : P.torque_max);
+      }
+      float s, c;
+      sincos_contract(E.ang[i], &s, &c);
+      fx[i] = 0.0f + (c * F[0] + (-s) * F[1]);
+      fy[i] = 0.0f + (s * F[0] + c * F[1]);
+      tq[i] = F[2];
+    }
+    unsigned long long ovf = 0;
+    physics_step(S, P, e, E, fx, fy, tq, L, lane, &ovf);
+    if (ovf) atomicAdd(&ctr->overflow, ovf);
 
-  // goal detection (game.py:401-412)
-  int goal = 0;
-  const float bx = E.px[4], by = E.py[4];
-  if (bx < 10.0f && 225.0f < by && by < 375.0f) { goal = 2; E.score_red += 1; }
-  else if (bx > 790.0f && 225.0f < by && by < 375.0f) { goal = 1; E.score_blue += 1; }
-  const bool done = P.max_steps > 0 && E.steps >= P.max_steps;
-  float r = blue_reward(P, pvx, pvy, E.px, E.py, goal, false, 0, 0);
-  bool rng_dirty = false;
-  if (goal) {
-    load_rng(S, e, E);
-    rng_dirty = true;
-    soft_reset_regs(E);
+    // goal detection (game.py:401-412)
+    int goal = 0;
+    const float bx = E.px[4], by = E.py[4];
+    if (bx < 10.0f && 225.0f < by && by < 375.0f) { goal = 2; E.score_red += 1; }
+    else if (bx > 790.0f && 225.0f < by && by < 375.0f) { goal = 1; E.score_blue += 1; }
+    const bool done = P.max_steps > 0 && E.steps >= P.max_steps;
+    float r = blue_reward(P, pvx, pvy, E.px, E.py, goal, false, 0, 0);
+    if (goal) {
+      load_rng(S, e, E);
+      rng_dirty = true;
+      soft_reset_regs(E);
+    }
+    if (done) r = blue_reward(P, pvx, pvy, E.px, E.py, goal, true, E.score_blue, E.score_red);
+
+    // outputs of this step (before a vec auto-reset)
+    if (rew) *(float4*)(rew + e * 4) = make_float4(r, r, 0.0f, 0.0f);
+    if (term) *(uint32_t*)(term + e * 4) = 0u;
+    if (trunc) *(uint32_t*)(trunc + e * 4) = done ? 0x01010101u : 0u;
+    if (goal_out) goal_out[e] = (int8_t)goal;
+    if (score_out) *(int2*)(score_out + e * 2) = make_int2(E.score_blue, E.score_red);
+
+    fill3 = (E.meta & META_HE) != 0;
+    if (done && P.autoreset) {
+      // marl_vecenv.py:48-51: env.reset(options={"use_full_random_positions": True})
+      if (!rng_dirty) load_rng(S, e, E);
+      rng_dirty = true;
+      reset_env_regs(E, MS_SPAWN_FULL_RANDOM);
+      fill3 = true;
+    }
   }
-  if (done) r = blue_reward(P, pvx, pvy, E.px, E.py, goal, true, E.score_blue, E.score_red);
-
-  // outputs of this step (before a vec auto-reset)
-  if (rew) *(float4*)(rew + e * 4) = make_float4(r, r, 0.0f, 0.0f);
-  if (term) *(uint32_t*)(term + e * 4) = 0u;
-  if (trunc) *(uint32_t*)(trunc + e * 4) = done ? 0x01010101u : 0u;
-  if (goal_out) goal_out[e] = (int8_t)goal;
-  if (score_out) *(int2*)(score_out + e * 2) = make_int2(E.score_blue, E.score_red);
-
-  if (done && P.autoreset) {
-    // marl_vecenv.py:48-51: env.reset(options={"use_full_random_positions": True})
-    if (!rng_dirty) load_rng(S, e, E);
-    rng_dirty = true;
-    reset_env_regs(E, MS_SPAWN_FULL_RANDOM);
-    emit_frames(S, P, e, E, true, obs);
-  } else {
-    emit_frames(S, P, e, E, (E.meta & META_HE) != 0, obs);
+  __syncthreads();  // LDS physics scratch -> obs staging
+  emit_frames(S, P, e, E, active, fill3, obs, L, lane, row_mask, e0);
+  if (active) {
+    if (rng_dirty) store_rng(S, e, E);
+    store_bodies(S, e, E);
+    store_scalars(S, e, E);
   }
-  if (rng_dirty) store_rng(S, e, E);
-  store_bodies(S, e, E);
-  store_scalars(S, e, E);
 }
 
 __global__ __launch_bounds__(MS_BLOCK) void ms_reset_kernel(DevState S, Params P, const uint64_t* __restrict__ pcg,
                                                             const uint8_t* __restrict__ mask, int mode, int set_hist_empty,
                                                             float* __restrict__ obs) {
-  const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + threadIdx.x;
-  if (e >= S.n) return;
-  if (mask && !mask[e]) return;
+  __shared__ Lds L;
+  const int lane = threadIdx.x;
+  const int64_t e0 = (int64_t)blockIdx.x * MS_BLOCK;
+  const int64_t e = e0 + lane;
+  const bool active = e < S.n && (!mask || mask[e]);
+  const uint64_t row_mask = __ballot(active);
   Env E;
-  load_scalars(S, e, E);
-  if (pcg) {
-    E.rng.shi = pcg[e * 4 + 0]; E.rng.slo = pcg[e * 4 + 1];
-    E.rng.ihi = pcg[e * 4 + 2]; E.rng.ilo = pcg[e * 4 + 3];
-    E.rng.has32 = 0; E.rng.u32 = 0;
-  } else {
-    load_rng(S, e, E);
+  if (active) {
+    load_scalars(S, e, E);
+    if (pcg) {
+      E.rng.shi = pcg[e * 4 + 0]; E.rng.slo = pcg[e * 4 + 1];
+      E.rng.ihi = pcg[e * 4 + 2]; E.rng.ilo = pcg[e * 4 + 3];
+      E.rng.has32 = 0; E.rng.u32 = 0;
+    } else {
+      load_rng(S, e, E);
+    }
+    reset_env_regs(E, mode);
   }
-  reset_env_regs(E, mode);
-  emit_frames(S, P, e, E, true, obs);
-  if (set_hist_empty) E.meta |= META_HE;
-  store_rng(S, e, E);
-  store_bodies(S, e, E);
-  store_scalars(S, e, E);
+  emit_frames(S, P, e, E, active, true, obs, L, lane, row_mask, e0);
+  if (active) {
+    if (set_hist_empty) E.meta |= META_HE;
+    store_rng(S, e, E);
+    store_bodies(S, e, E);
+    store_scalars(S, e, E);
+  }
 }
 
 __global__ __launch_bounds__(MS_BLOCK) void ms_observe_kernel(DevState S, Params P, float* __restrict__ frames) {

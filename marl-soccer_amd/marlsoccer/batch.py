@@ -141,6 +141,26 @@ class SoccerBatch:
             N.check(self._L.ms_step(self._h, self._ptr(actions), self._ptr(obs), self._ptr(rew), self._ptr(term),
                                     self._ptr(trunc), self._ptr(goal), self._ptr(score)), "ms_step")
 
+    def launcher(self, actions: list, obs: torch.Tensor, rew=None, term=None, trunc=None, goal=None, score=None):
+        """Pre-bound ms_step for a hot loop: returns f(i) that steps with actions[i % len]
+        into the given tensors. All argument conversion happens once, here; each call is
+        one ctypes call (no device switch: call from the env's current device)."""
+        if torch.cuda.current_device() != self.device.index:
+            raise RuntimeError("launcher(): make the env's device current (torch.cuda.set_device)")
+        fn, h = self._L.ms_step, self._h
+        outs = tuple(self._ptr(t) for t in (obs, rew, term, trunc, goal, score))
+        acts = [self._ptr(a.contiguous()) for a in actions]
+        keep = (actions, obs, rew, term, trunc, goal, score)
+        n = len(acts)
+
+        def step(i: int) -> None:
+            rc = fn(h, acts[i % n], *outs)
+            if rc:
+                N.check(rc, "ms_step")
+
+        step._keepalive = keep  # the tensors must outlive the pointers
+        return step
+
     def observe(self) -> torch.Tensor:
         """Current frame of every agent, (N, 4, 22) (Game._get_observations)."""
         out = torch.empty((self.num_envs, 4, 22), dtype=torch.float32, device=self.device)

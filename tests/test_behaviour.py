@@ -1,0 +1,186 @@
+"""Behavioural acceptance tests on the GPU env — the scenarios of the reference's
+soccer_simulation/test_rewards.py (main(), :614-635), re-expressed with scripted
+controllers that read the observation exactly as the reference's do (world vectors from
+unit x magnitude x field diagonal, agent angle = obs[2] * pi).
+
+These are the only reference-side checks that depend on the physics, and they depend on
+it only qualitatively (signs and thresholds), so they pin behaviour, not numerics.
+"""
+import math
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+BALL, OWN_GOAL, OPP_GOAL = 13, 16, 19
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+
+
+def latest(o):
+    return o[44:66]
+
+
+def vec_from(frame, start):
+    return frame[start:start + 2].astype(np.float64) * float(frame[start + 2]) * 1000.0
+
+
+def to_local(v, angle):
+    c, s = math.cos(angle), math.sin(angle)
+    return np.array([v[0] * c + v[1] * s, -v[0] * s + v[1] * c])
+
+
+def toward(v, angle):
+    d = to_local(v, angle)
+    n = np.linalg.norm(d)
+    d = d / n if n > 1e-8 else d
+    return np.array([d[0], d[1], 0.0], np.float32)
+
+
+def zeros(env):
+    return {a: np.zeros(3, np.float32) for a in env.possible_agents}
+
+
+def make_env(**rewards):
+    from marlsoccer.config import load_config
+    from soccer_env import soccerenv
+    c = load_config()
+    c["rewards"].update(rewards)
+    return soccerenv(config=c)
+
+
+def test_baseline_zero_action_reward_is_alive_penalty():
+    env = make_env()
+    env.reset(seed=1)
+    _, rew, _, _, _ = env.step(zeros(env))
+    assert rew["agent_0"] == rew["agent_1"] == float(np.float32(-0.00001))
+    env.close()
+
+
+@pytest.mark.parametrize("agent", [0, 1])
+@pytest.mark.parametrize("sign", [+1, -1])
+def test_proximity_shaping_sign(agent, sign):
+    """test_rewards.py:139-199: 6 steps toward (away from) the ball beat (trail) 6x the
+    zero-action baseline."""
+    env = make_env()
+    env.reset(seed=10 + agent)
+    obs, base, _, _, _ = env.step(zeros(env))
+    total = 0.0
+    for _ in range(6):
+        f = latest(obs[f"agent_{agent}"])
+        ball = vec_from(f, BALL)
+        acts = zeros(env)
+        acts[f"agent_{agent}"] = toward(sign * ball, f[2] * math.pi)
+        obs, rew, _, _, _ = env.step(acts)
+        total += rew[f"agent_{agent}"]
+    delta = total - 6 * base[f"agent_{agent}"]
+    assert (delta > 0) if sign > 0 else (delta < 0), delta
+    env.close()
+
+
+def test_push_ball_toward_red_goal_is_rewarded():
+    """test_rewards.py:202-251: approach the ball (<= 60 steps), push 5 steps toward the
+    red goal; the cumulative blue reward is positive."""
+    env = make_env()
+    env.reset(seed=5, options={"use_fixed_positions": True})
+    obs, _, _, _, _ = env.step(zeros(env))
+    total = 0.0
+    for _ in range(60):
+        f = latest(obs["agent_0"])
+        ball = vec_from(f, BALL)
+        if np.linalg.norm(ball) < 35.0:
+            break
+        acts = zeros(env)
+        acts["agent_0"] = toward(ball, f[2] * math.pi)
+        obs, rew, _, trunc, info = env.step(acts)
+        total += rew["agent_0"] + rew["agent_1"]
+        assert "goal_scored_by" not in info["agent_0"] and not any(trunc.values())
+    for _ in range(5):
+        f = latest(obs["agent_0"])
+        acts = zeros(env)
+        acts["agent_0"] = toward(vec_from(f, OPP_GOAL), f[2] * math.pi)
+        obs, rew, _, _, info = env.step(acts)
+        total += rew["agent_0"] + rew["agent_1"]
+    assert total > 0, total
+    env.close()
+
+
+def dribble(env, obs, agent, target_goal, steps):
+    """Stand behind the ball on the line to `target_goal` (world vector from the obs) and
+    push through it; returns (obs, rewards list, goal_scored_by or None, done)."""
+    rews = []
+    for _ in range(steps):
+        f = latest(obs[f"agent_{agent}"])
+        ang = f[2] * math.pi
+        ball = vec_from(f, BALL)
+        goal = vec_from(f, target_goal)
+        g_dir = (goal - ball) / (np.linalg.norm(goal - ball) + 1e-9)
+        behind = ball - 24.0 * g_dir
+        if np.linalg.norm(behind) < 6.0 or (np.dot(ball, g_dir) > 0 and np.linalg.norm(ball) < 30):
+            move = ball + 20.0 * g_dir
+        else:
+            move = behind
+        acts = zeros(env)
+        acts[f"agent_{agent}"] = toward(move, ang)
+        obs, rew, _, trunc, info = env.step(acts)
+        rews.append(rew["agent_0"] + rew["agent_1"])
+        if "goal_scored_by" in info["agent_0"]:
+            return obs, rews, info["agent_0"]["goal_scored_by"], any(trunc.values())
+        if any(trunc.values()):
+            return obs, rews, None, True
+    return obs, rews, None, False
+
+
+@pytest.mark.parametrize("agent", [0, 1])
+def test_goal_scored_then_terminal_reward(agent):
+    """test_rewards.py:415-516: blue scores; the goal step carries +goal_scored_reward;
+    the terminal step's reward is score_difference_multiplier * (blue - red)."""
+    env = make_env(score_difference_multiplier=5.0)
+    obs, _ = env.reset(seed=7 + agent, options={"use_fixed_positions": True})
+    obs, rews, who, done = dribble(env, obs, agent, OPP_GOAL, 990)
+    assert who == "blue" and not done, (who, done, len(rews))
+    assert rews[-1] > 2 * 3.9  # both blue agents get +4 plus shaping
+    last = None
+    while env.agents:
+        obs, rew, _, trunc, info = env.step(zeros(env))
+        last = rew, info
+    rew, info = last
+    diff = info["agent_0"]["score"]["blue"] - info["agent_0"]["score"]["red"]
+    assert diff >= 1 and rew["agent_0"] == rew["agent_1"] == 5.0 * diff
+    env.close()
+
+
+def test_own_goal_is_conceded_and_penalised():
+    """test_rewards.py:254-363 / 519-612: blue pushes the ball into its own goal; red is
+    credited and the blue episode reward is negative."""
+    env = make_env(goal_conceded_penalty=1.0)
+    obs, _ = env.reset(seed=3, options={"use_fixed_positions": True})
+    obs, rews, who, done = dribble(env, obs, 0, OWN_GOAL, 990)
+    assert who == "red" and not done, (who, len(rews))
+    assert rews[-1] < -2 * 0.9 and sum(rews) < 0
+    env.close()
+
+
+def test_random_play_returns_match_reference_scale():
+    """Notebook cell 0 (marl-soccer.ipynb JSON L13-27): 5 random-action episodes with
+    full-random spawns score 0-0 with small positive/negative blue returns (0.15-1.28)."""
+    env = make_env()
+    rng = np.random.default_rng(0)
+    rets = []
+    for ep in range(5):
+        env.reset(seed=100 + ep, options={"use_full_random_positions": True})
+        ret, goals = 0.0, 0
+        while env.agents:
+            acts = {a: rng.uniform(-1, 1, 3).astype(np.float32) for a in env.agents}
+            _, rew, _, _, info = env.step(acts)
+            ret += rew["agent_0"]
+            goals += "goal_scored_by" in info["agent_0"]
+        rets.append(ret)
+    assert all(abs(r) < 5.0 for r in rets), rets
+    env.close()

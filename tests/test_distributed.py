@@ -1,0 +1,86 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the env-sharding contract.
+
+The GPU path shards envs across ranks with no data-path collective; env g is seeded
+seed + g and driven by actions that are a function of its global index, so a sharded run
+must equal a single-process run bit for bit. Here the fp32 oracle stands in for each
+rank's GPU batch (no GPU on this host) and gloo stands in for RCCL; the shard arithmetic
+and the gather layout are the product's (marlsoccer.distributed).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from marlsoccer.distributed import shard_range  # noqa: E402
+
+
+def test_shard_range_partitions_exactly():
+    for g in (1, 7, 64, 65536, 262144, 100003):
+        for w in (1, 2, 3, 4, 8):
+            spans = [shard_range(g, w, r) for r in range(w)]
+            assert spans[0][0] == 0
+            for (s0, c0), (s1, _) in zip(spans, spans[1:]):
+                assert s0 + c0 == s1
+            assert sum(c for _, c in spans) == g
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, G, steps, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "tests"), os.path.join(root, "oracle"), os.path.join(root, "marl-soccer_amd")]
+    import oracle as orc
+    import sim_helpers as sh
+    from marlsoccer.distributed import shard_range as sr
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    start, count = sr(G, world, rank)
+    env = orc.OracleBatch(count, "f32", orc.default_config(max_steps=40))
+    env.reset(np.stack([orc.pcg_from_seed(19 + start + i) for i in range(count)]), 0)
+    for t in range(steps):
+        obs = env.step(sh.hash_actions(count, t, env0=start))[0]
+    parts = [torch.empty((count, 4, 66)) for _ in range(world)]
+    dist.all_gather(parts, torch.from_numpy(obs))
+    elapsed = torch.tensor([float(rank + 1)])
+    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)  # bench.py's max-over-ranks timing
+    if rank == 0:
+        q.put((torch.cat(parts).numpy(), float(elapsed)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_equals_single_process():
+    import oracle as orc
+    import sim_helpers as sh
+
+    G, steps, world = 64, 90, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, G, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered, tmax = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert tmax == 2.0
+    single = orc.OracleBatch(G, "f32", orc.default_config(max_steps=40))
+    single.reset(np.stack([orc.pcg_from_seed(19 + i) for i in range(G)]), 0)
+    for t in range(steps):
+        obs = single.step(sh.hash_actions(G, t))[0]
+    np.testing.assert_array_equal(gathered, obs)
