@@ -144,9 +144,14 @@ typedef struct ms_arbiter_state {
   float jt[2];     /* accumulated tangent impulse */
 } ms_arbiter_state;
 
+/* Obs history is kept as state snapshots: the 22-float frame of every agent is a pure
+ * function of these 26 values (Game._get_observations, game.py:258-322), so the frames of
+ * t-2 and t-1 are recomputed bit-identically instead of being stored. */
+#define MS_SNAP_SIZE 26 /* px[5], py[5], vx[4], vy[4], angle[4], w[4] (agents 0..3, ball 4) */
+
 typedef struct ms_env_state {
   ms_body_state body[MS_N_BODIES];
-  float frames[2][MS_N_AGENTS][MS_FRAME_SIZE]; /* obs history: [0] = t-2, [1] = t-1 */
+  float snap[2][MS_SNAP_SIZE]; /* obs history snapshots: [0] = t-2, [1] = t-1 */
   int32_t steps;
   int32_t score_blue;
   int32_t score_red;

@@ -8,7 +8,7 @@
 //
 // HBM layout (struct-of-arrays, every plane is N contiguous elements so a wavefront's
 // 64 lanes touch 64 consecutive words):
-//   F  float [PL_F][N]   bodies (44 planes) + 3-frame history ring (2 x 4 x 22 planes)
+//   F  float [PL_F][N]   bodies (44 planes) + obs-history snapshot ring (2 x 26 planes)
 //   I  int32 [PL_I][N]   steps, score, meta bits, PCG64 buffered u32
 //   R  u64   [4][N]      PCG64 state/increment (touched only by resets and goal respawns)
 //   CH u32   [2][MAXA][N] arbiter-cache headers, ping-pong by a per-env parity bit
@@ -24,6 +24,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <type_traits>
 
 #include "ms_device.h"
 
@@ -41,8 +42,8 @@ using namespace ms;
 enum {
   // agent b (0..3): base b*9: PX PY VX VY ANG W VBX VBY WB ; ball: base 36: PX PY VX VY W VBX VBY WB
   F_BALL = 36,
-  F_HIST = 44,            // [slot 2][agent 4][22]
-  PL_F = 44 + 2 * 4 * 22  // 220
+  F_SNAP = 44,                   // [slot 2][MS_SNAP_SIZE]: px[5] py[5] vx[4] vy[4] angle[4] w[4]
+  PL_F = 44 + 2 * MS_SNAP_SIZE   // 96
 };
 enum { I_STEPS = 0, I_SCORE = 1, I_META = 2, I_U32 = 3, PL_I = 4 };
 // META bits: 0-1 spawn mode, 2 hist_empty, 3 ring head (slot holding t-1), 4 cache parity,
@@ -55,6 +56,7 @@ enum { I_STEPS = 0, I_SCORE = 1, I_META = 2, I_U32 = 3, PL_I = 4 };
 #define META_H32 (1u << 16)
 
 struct DevState {
+  unsigned long long* stamps;  // MS_STAMPS diagnostic builds only: [wave][16] s_memtime
   float* F;
   int32_t* I;
   uint64_t* R;
@@ -70,6 +72,16 @@ struct Counters {
 };
 
 __device__ __forceinline__ float& AGF(const DevState& S, int b, int f, int64_t e) { return S.F[(int64_t)(b * 9 + f) * S.n + e]; }
+
+#ifdef MS_STAMPS
+#define STAMP(k)                                                                         \
+  do {                                                                                   \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
+    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[(int64_t)(blockIdx.x) * 16 + (k)] = t_; \
+  } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
 
 // ---- per-lane env register file ------------------------------------------------------------
 struct Env {
@@ -131,16 +143,13 @@ __device__ __forceinline__ void store_rng(const DevState& S, int64_t e, Env& E) 
 // body/box each lane selects, so dynamic per-lane indexing is bank-conflict free.
 enum { SV_VX = 0, SV_VY, SV_W, SV_VBX, SV_VBY, SV_WB, SV_PX, SV_PY, SV_N };
 enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
-#define OBS_LD 67  // padded obs staging row: lanes l and l+16 fall in different banks
 
 struct Lds {
-  union {
-    struct {
-      float v[SV_N][6][MS_BLOCK];    // body p, v, w, v_bias, w_bias (body 5 = static, all 0)
-      float box[BX_N][4][MS_BLOCK];  // agent box transform (p, cos, sin)
-    } ph;
-    float obs[MS_BLOCK][OBS_LD];     // one agent's 66-float obs row per env, staged for stores
-  };
+  Seg seg[8];  // static segments (walls, goal lines), read with per-lane indices
+  struct {
+    float v[SV_N][6][MS_BLOCK];    // body p, v, w, v_bias, w_bias (body 5 = static, all 0)
+    float box[BX_N][4][MS_BLOCK];  // agent box transform (p, cos, sin)
+  } ph;
 };
 
 // ---- frames -----------------------------------------------------------------------------
@@ -153,58 +162,100 @@ __device__ __forceinline__ void frame_of(const Params& P, const Env& E, int agen
   }
 }
 
-// Stacked obs [t-2, t-1, t] per agent (soccer_env.py:130-140) and the history ring update;
-// fill3: all three slots are the new frame (reset, soccer_env.py:90-96). Rows are staged in
-// LDS and written cooperatively by the whole wave (each store instruction covers two
-// consecutive 264-B rows instead of 64 rows 1056 B apart). Every lane of the block must call
-// this; `active` lanes contribute rows, `row_mask` selects which rows are stored.
-__device__ __forceinline__ void emit_frames(const DevState& S, const Params& P, int64_t e, Env& E, bool active,
-                                            bool fill3, float* __restrict__ obs, Lds& L, int lane,
-                                            uint64_t row_mask, int64_t e0) {
-  const int64_t n = S.n;
-  const int head = (E.meta & META_RING) ? 1 : 0;  // slot holding t-1; the other holds t-2
-  const int old = head ^ 1;
-#pragma unroll 1
-  for (int a = 0; a < 4; ++a) {
-    if (active) {
-      float f[22];
-      frame_of(P, E, a, f);
-      float* row = L.obs[lane];
-      if (fill3) {
+// Snapshot of the obs inputs (include/marl_soccer.h MS_SNAP_SIZE)
+struct Snap {
+  float px[5], py[5], vx[4], vy[4], ang[4], w[4];
+};
+__device__ __forceinline__ void snap_of(const Env& E, Snap& s) {
 #pragma unroll
-        for (int k = 0; k < 22; ++k) {
-          S.F[(int64_t)(F_HIST + 0 * 88 + a * 22 + k) * n + e] = f[k];
-          S.F[(int64_t)(F_HIST + 1 * 88 + a * 22 + k) * n + e] = f[k];
-          row[k] = f[k]; row[22 + k] = f[k]; row[44 + k] = f[k];
-        }
-      } else {
-        float* ho = S.F + (int64_t)(F_HIST + old * 88 + a * 22) * n + e;
-        float* hn = S.F + (int64_t)(F_HIST + head * 88 + a * 22) * n + e;
-        float t2[22], t1[22];
+  for (int b = 0; b < 5; ++b) { s.px[b] = E.px[b]; s.py[b] = E.py[b]; }
 #pragma unroll
-        for (int k = 0; k < 22; ++k) { t2[k] = ho[k * n]; t1[k] = hn[k * n]; }
+  for (int i = 0; i < 4; ++i) { s.vx[i] = E.vx[i]; s.vy[i] = E.vy[i]; s.ang[i] = E.ang[i]; s.w[i] = E.w[i]; }
+}
+__device__ __forceinline__ void snap_load(const DevState& S, int64_t e, int slot, Snap& s) {
+  const float* p = S.F + (int64_t)(F_SNAP + slot * MS_SNAP_SIZE) * S.n + e;
 #pragma unroll
-        for (int k = 0; k < 22; ++k) {
-          row[k] = t2[k]; row[22 + k] = t1[k]; row[44 + k] = f[k];
-          ho[k * n] = f[k];  // new frame replaces t-2
-        }
-      }
-    }
-    __syncthreads();
-    if (obs) {
-      // 64 rows x 33 float2 per agent; consecutive lanes store consecutive float2 of a row
-#pragma unroll 1
-      for (int q = lane; q < MS_BLOCK * 33; q += MS_BLOCK) {
-        const int r = q / 33, k2 = q - r * 33;
-        if ((row_mask >> r) & 1ull)
-          *(float2*)(obs + (e0 + r) * 264 + a * 66 + 2 * k2) = make_float2(L.obs[r][2 * k2], L.obs[r][2 * k2 + 1]);
-      }
-    }
-    __syncthreads();
+  for (int b = 0; b < 5; ++b) { s.px[b] = p[(int64_t)b * S.n]; s.py[b] = p[(int64_t)(5 + b) * S.n]; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s.vx[i] = p[(int64_t)(10 + i) * S.n]; s.vy[i] = p[(int64_t)(14 + i) * S.n];
+    s.ang[i] = p[(int64_t)(18 + i) * S.n]; s.w[i] = p[(int64_t)(22 + i) * S.n];
   }
-  if (active) {
-    if (fill3) E.meta &= ~(META_HE | META_RING);
-    else E.meta ^= META_RING;
+}
+__device__ __forceinline__ void snap_store(const DevState& S, int64_t e, int slot, const Snap& s) {
+  float* p = S.F + (int64_t)(F_SNAP + slot * MS_SNAP_SIZE) * S.n + e;
+#pragma unroll
+  for (int b = 0; b < 5; ++b) { p[(int64_t)b * S.n] = s.px[b]; p[(int64_t)(5 + b) * S.n] = s.py[b]; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p[(int64_t)(10 + i) * S.n] = s.vx[i]; p[(int64_t)(14 + i) * S.n] = s.vy[i];
+    p[(int64_t)(18 + i) * S.n] = s.ang[i]; p[(int64_t)(22 + i) * S.n] = s.w[i];
+  }
+}
+template <int A>
+__device__ __forceinline__ void snap_frame(const Params& P, const Snap& s, float* o) {
+  agent_frame<A>(P, s.px, s.py, s.vx, s.vy, s.ang, s.w, o);
+}
+
+// One 22-float frame of the 528-B block of an agent pair (soccer_env.py:130-140 stacks
+// [t-2, t-1, t] per agent). Frame K (0..5) = agent 2*PAIR + K/3, snapshot K%3. Frames start
+// 88 B apart, so even frames are 16-B aligned: five float4 stores plus a 2-float carry that
+// the next (odd) frame completes, i.e. 33 float4 stores per pair with 24 live floats.
+template <int PAIR, int K>
+__device__ __forceinline__ void store_obs_frame(const Params& P, const Snap& s2, const Snap& s1, const Snap& s0,
+                                                float4* __restrict__ d, float& c0, float& c1) {
+  constexpr int A = 2 * PAIR + K / 3;
+  const Snap& s = (K % 3 == 0) ? s2 : ((K % 3 == 1) ? s1 : s0);
+  float f[22];
+  snap_frame<A>(P, s, f);
+  if constexpr ((K & 1) == 0) {
+    const int q0 = (22 * K) / 4;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) d[q0 + q] = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
+    c0 = f[20]; c1 = f[21];
+  } else {
+    const int q0 = (22 * K - 2) / 4;
+    d[q0] = make_float4(c0, c1, f[0], f[1]);
+#pragma unroll
+    for (int q = 0; q < 5; ++q) d[q0 + 1 + q] = make_float4(f[2 + 4 * q], f[3 + 4 * q], f[4 + 4 * q], f[5 + 4 * q]);
+  }
+}
+
+template <int PAIR>
+__device__ __forceinline__ void store_obs_pair(const Params& P, const Snap& s2, const Snap& s1, const Snap& s0,
+                                               float* __restrict__ dst) {
+  float4* d = (float4*)dst;
+  float c0, c1;
+  store_obs_frame<PAIR, 0>(P, s2, s1, s0, d, c0, c1);
+  store_obs_frame<PAIR, 1>(P, s2, s1, s0, d, c0, c1);
+  store_obs_frame<PAIR, 2>(P, s2, s1, s0, d, c0, c1);
+  store_obs_frame<PAIR, 3>(P, s2, s1, s0, d, c0, c1);
+  store_obs_frame<PAIR, 4>(P, s2, s1, s0, d, c0, c1);
+  store_obs_frame<PAIR, 5>(P, s2, s1, s0, d, c0, c1);
+}
+
+// Obs output + history ring update. fill3: all three frames are the current one (reset,
+// soccer_env.py:90-96). Only the current snapshot is written back (26 floats), into the
+// slot that held t-2.
+__device__ __forceinline__ void emit_frames(const DevState& S, const Params& P, int64_t e, Env& E, bool fill3,
+                                            const Snap& s2_in, const Snap& s1_in, float* __restrict__ obs) {
+  Snap s0;
+  snap_of(E, s0);
+  const int head = (E.meta & META_RING) ? 1 : 0;  // slot holding t-1; the other holds t-2
+  const Snap& s2 = fill3 ? s0 : s2_in;
+  const Snap& s1 = fill3 ? s0 : s1_in;
+  if (obs && MS_ABLATE != 3) {
+    float* dst = obs + e * 264;
+    store_obs_pair<0>(P, s2, s1, s0, dst);
+    store_obs_pair<1>(P, s2, s1, s0, dst + 132);
+  }
+  if (fill3) {
+    snap_store(S, e, 0, s0);
+    snap_store(S, e, 1, s0);
+    E.meta &= ~(META_HE | META_RING);
+  } else {
+    snap_store(S, e, head ^ 1, s0);  // new t-1
+    E.meta ^= META_RING;
   }
 }
 
@@ -232,6 +283,16 @@ __device__ __forceinline__ void soft_reset_regs(Env& E) {
     E.ang[b] = b < 2 ? 0.0f : 3.14159265358979323846f;
   }
   E.vx[4] = 0.0f; E.vy[4] = 0.0f;
+}
+
+// copy the segment table from the kernel arguments with constant indices (a per-lane index
+// into the by-value Params would make the compiler copy all of Params to scratch)
+__device__ __forceinline__ void stage_segments(const Params& P, Lds& L, int lane) {
+  if (lane == 0) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) L.seg[s] = P.seg[s];
+  }
+  __syncthreads();
 }
 
 // ---- physics: cpSpaceStep restated ---------------------------------------------------------
@@ -268,26 +329,54 @@ __device__ __forceinline__ void cache_write(const DevState& S, int par, int k, i
 // Per-lane working set of the contact pipeline.
 struct Contacts {
   CSlot reg[KREG];
-  CSlot* ovf;  // overflow slots KREG..MAXC-1 (private memory; only pile-ups reach it)
   int nc, na;
 };
 
-__device__ __forceinline__ void slot_put(Contacts& C, int k, const CSlot& s) {
-  if (k < KREG) {
-#pragma unroll
-    for (int q = 0; q < KREG; ++q)
-      if (q == k) C.reg[q] = s;
-  } else {
-    C.ovf[k - KREG] = s;
+// Compile-time loop: every reg[] access below uses a constant index from the first IR on,
+// so the slots are promoted to registers (an unrolled runtime loop is not: SROA runs first).
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
   }
+}
+
+// d = c ? s : d, field by field with unconditional stores: a conditional whole-struct store
+// lets the optimizer merge the KREG stores into one store through a phi of slot pointers,
+// which pins the slots in scratch memory.
+__device__ __forceinline__ void slot_select(CSlot& d, const CSlot& s, bool c) {
+  d.r1x = c ? s.r1x : d.r1x; d.r1y = c ? s.r1y : d.r1y; d.r2x = c ? s.r2x : d.r2x; d.r2y = c ? s.r2y : d.r2y;
+  d.nx = c ? s.nx : d.nx; d.ny = c ? s.ny : d.ny; d.u = c ? s.u : d.u;
+  d.nMass = c ? s.nMass : d.nMass; d.tMass = c ? s.tMass : d.tMass; d.bias = c ? s.bias : d.bias;
+  d.bounce = c ? s.bounce : d.bounce; d.jn = c ? s.jn : d.jn; d.jt = c ? s.jt : d.jt; d.jb = c ? s.jb : d.jb;
+  d.m = c ? s.m : d.m;
+}
+
+// overflow slots KREG..MAXC-1 live in private memory; only pile-ups reach them
+__device__ __forceinline__ void slot_put(Contacts& C, CSlot* ovf, int k, const CSlot& s) {
+  static_for<0, KREG>([&](auto qc) __attribute__((always_inline)) {
+    constexpr int q = decltype(qc)::value;
+    slot_select(C.reg[q], s, q == k);
+  });
+  if (k >= KREG) ovf[k - KREG] = s;
+}
+
+// per-body inverse mass / moment without a per-lane indexed parameter load
+__device__ __forceinline__ float body_minv(const Params& P, int b) {
+  return b < 4 ? P.m_inv[0] : (b == 4 ? P.m_inv[4] : 0.0f);
+}
+__device__ __forceinline__ float body_iinv(const Params& P, int b) {
+  return b < 4 ? P.i_inv[0] : (b == 4 ? P.i_inv[4] : 0.0f);
 }
 
 // cpArbiterPreStep for one contact (velocities: previous step's post-solve values)
 __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds& L, int lane) {
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
-  const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
+  const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_minv(P, bb), ib = body_iinv(P, bb);
   const int p = CS_PAIR(c.m);
-  const float e = p < 6 ? P.e_aa : (p < 10 ? P.e_ab : (p < 42 ? (((p - 10) & 7) < 6 ? P.e_aw : P.e_ag) : P.e_bw));
+  const float e_s = ((p - 10) & 7) < 6 ? P.e_aw : P.e_ag;
+  const float e = p < 6 ? P.e_aa : (p < 10 ? P.e_ab : (p < 42 ? e_s : P.e_bw));
   const V2 n = v2(c.nx, c.ny);
   const V2 body_delta = v2(L.ph.v[SV_PX][bb][lane] - L.ph.v[SV_PX][ba][lane], L.ph.v[SV_PY][bb][lane] - L.ph.v[SV_PY][ba][lane]);
   const V2 va = v2(L.ph.v[SV_VX][ba][lane], L.ph.v[SV_VY][ba][lane]);
@@ -311,7 +400,7 @@ __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds
 __device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L, int lane) {
   if (!CS_WARM(c.m)) return;
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
-  const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
+  const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_minv(P, bb), ib = body_iinv(P, bb);
   const V2 j = vrotate(v2(c.nx, c.ny), v2(c.jn, c.jt));
   const V2 nj = vneg(j);
   L.ph.v[SV_VX][ba][lane] = L.ph.v[SV_VX][ba][lane] + nj.x * ma;
@@ -325,7 +414,7 @@ __device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L
 // cpArbiterApplyImpulse for one contact
 __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int lane) {
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
-  const float ma = P.m_inv[ba], ia = P.i_inv[ba], mb = P.m_inv[bb], ib = P.i_inv[bb];
+  const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_minv(P, bb), ib = body_iinv(P, bb);
   const V2 n = v2(c.nx, c.ny);
   const V2 r1 = v2(c.r1x, c.r1y), r2 = v2(c.r2x, c.r2y);
   const float vbxa = L.ph.v[SV_VBX][ba][lane], vbya = L.ph.v[SV_VBY][ba][lane], wba = L.ph.v[SV_WB][ba][lane];
@@ -409,7 +498,7 @@ __device__ __forceinline__ void cache_age_current(const DevState& S, int64_t e, 
 
 // cpSpaceCollideShapes + cpArbiterUpdate for one touching pair
 __device__ __forceinline__ void add_arbiter(const DevState& S, int64_t e, const Lds& L, int lane, Contacts& C,
-                                            CacheWalk& W, int p, int ba, int bb, const Col& col, float u,
+                                            CSlot* ovf, CacheWalk& W, int p, int ba, int bb, const Col& col, float u,
                                             unsigned long long* overflow_acc) {
   if (C.na >= MAXA) { (*overflow_acc)++; return; }
   while (W.cur < W.nc_old && (int)(W.curh & 63u) < p) cache_age_current(S, e, W, overflow_acc);
@@ -444,7 +533,7 @@ __device__ __forceinline__ void add_arbiter(const DevState& S, int64_t e, const 
     }
     s.m = (uint32_t)ba | ((uint32_t)bb << 3) | (warm << 6) | ((uint32_t)k << 7) | ((uint32_t)col.count << 8) |
           ((uint32_t)(h & 0xff) << 10) | ((uint32_t)pos << 18) | ((uint32_t)p << 24);
-    slot_put(C, C.nc, s);
+    slot_put(C, ovf, C.nc, s);
     C.nc++;
   }
 }
@@ -459,16 +548,17 @@ __device__ __forceinline__ void write_arbiter_cache(const DevState& S, int npar,
   cache_write(S, npar, CS_POS(c0.m), e, hdr, c0.jn, c0.jt, two ? c1.jn : 0.0f, two ? c1.jt : 0.0f);
 }
 
-#define FOR_CONTACTS(C, BODY)                                         \
+#define FOR_CONTACTS(C, OVF, BODY)                                    \
   {                                                                   \
-    _Pragma("unroll") for (int k_ = 0; k_ < KREG; ++k_) {             \
+    static_for<0, KREG>([&](auto kc_) __attribute__((always_inline)) {                             \
+      constexpr int k_ = decltype(kc_)::value;                        \
       if (k_ < (C).nc) {                                              \
         CSlot& c_ = (C).reg[k_];                                      \
         BODY;                                                         \
       }                                                               \
-    }                                                                 \
+    });                                                               \
     for (int k_ = KREG; k_ < (C).nc; ++k_) {                          \
-      CSlot& c_ = (C).ovf[k_ - KREG];                                 \
+      CSlot& c_ = (OVF)[k_ - KREG];                                   \
       BODY;                                                           \
     }                                                                 \
   }
@@ -511,6 +601,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
   const float ballbb[4] = {ballc.x - BR, ballc.y - BR, ballc.x + BR, ballc.y + BR};
 
   // broadphase: AABB masks per pair class (cpBBIntersects), no divergence
+  STAMP(2);
   uint32_t mAA = 0, mBA = 0, mSA = 0, mBS = 0;
   {
     const int AI[6] = {0, 0, 0, 1, 1, 2}, AJ[6] = {1, 2, 3, 2, 3, 3};
@@ -532,9 +623,8 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
   mAA = mBA = mSA = mBS = 0;
 #endif
 
-  CSlot ovf_store[MAXC - KREG];
+  CSlot ovf[MAXC - KREG];
   Contacts C;
-  C.ovf = ovf_store;
   C.nc = 0;
   C.na = 0;
   CacheWalk W;
@@ -556,7 +646,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     lds_box(L, j, lane, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     col_box_box(A, B, col);
-    if (col.count) add_arbiter(S, e, L, lane, C, W, p, i, j, col, P.u_aa, overflow_acc);
+    if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, p, i, j, col, P.u_aa, overflow_acc);
   }
   while (mBA) {
     const int i = __builtin_ctz(mBA);
@@ -565,7 +655,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     lds_box(L, i, lane, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     col_circle_box(ballc, BR, B, col);
-    if (col.count) add_arbiter(S, e, L, lane, C, W, 6 + i, 4, i, col, P.u_ab, overflow_acc);
+    if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, 6 + i, 4, i, col, P.u_ab, overflow_acc);
   }
   while (mSA) {
     const int q = __builtin_ctz(mSA);
@@ -574,20 +664,30 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     Box B;
     lds_box(L, i, lane, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
-    col_seg_box(P.seg[s], B, col);
-    if (col.count) add_arbiter(S, e, L, lane, C, W, 10 + q, 5, i, col, s < 6 ? P.u_aw : P.u_ag, overflow_acc);
+    const Seg sg = L.seg[s];
+    col_seg_box(sg, B, col);
+    if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, 10 + q, 5, i, col, s < 6 ? P.u_aw : P.u_ag, overflow_acc);
   }
   while (mBS) {
     const int s = __builtin_ctz(mBS);
     mBS &= mBS - 1;
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
-    col_circle_seg(ballc, BR, P.seg[s], col);
-    if (col.count) add_arbiter(S, e, L, lane, C, W, 42 + s, 4, 5, col, P.u_bw, overflow_acc);
+    const Seg sg = L.seg[s];
+    col_circle_seg(ballc, BR, sg, col);
+    if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, 42 + s, 4, 5, col, P.u_bw, overflow_acc);
   }
   while (W.cur < W.nc_old) cache_age_current(S, e, W, overflow_acc);
+  STAMP(3);
+#ifdef MS_STAMPS
+  {
+    int mx = C.nc;
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[(int64_t)blockIdx.x * 16 + 12] = (unsigned long long)mx;
+  }
+#endif
 
   // cpArbiterPreStep
-  FOR_CONTACTS(C, prestep_one(P, c_, L, lane));
+  FOR_CONTACTS(C, ovf, prestep_one(P, c_, L, lane));
 
   // cpBodyUpdateVelocity + entities.py velocity_func (damping, max-velocity clamp)
 #pragma unroll
@@ -610,27 +710,35 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     L.ph.v[SV_VX][b][lane] = nvx; L.ph.v[SV_VY][b][lane] = nvy; L.ph.v[SV_W][b][lane] = nw;
   }
 
+  STAMP(4);
   if (C.nc > 0) {
     // cpArbiterApplyCachedImpulse, then cpArbiterApplyImpulse x 10 (pymunk Space default)
-    FOR_CONTACTS(C, warm_one(P, c_, L, lane));
+    FOR_CONTACTS(C, ovf, warm_one(P, c_, L, lane));
 #pragma unroll 1
-    for (int it = 0; it < 10 * (MS_ABLATE != 1); ++it) FOR_CONTACTS(C, solve_one(P, c_, L, lane));
+    for (int it = 0; it < 10 * (MS_ABLATE != 1); ++it) {
+      asm volatile("; MS_SOLVER_ITER_BEGIN" ::: "memory");
+      FOR_CONTACTS(C, ovf, solve_one(P, c_, L, lane));
+      asm volatile("; MS_SOLVER_ITER_END" ::: "memory");
+    }
+    STAMP(5);
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
       E.vx[b] = L.ph.v[SV_VX][b][lane]; E.vy[b] = L.ph.v[SV_VY][b][lane]; E.w[b] = L.ph.v[SV_W][b][lane];
       E.vbx[b] = L.ph.v[SV_VBX][b][lane]; E.vby[b] = L.ph.v[SV_VBY][b][lane]; E.wb[b] = L.ph.v[SV_WB][b][lane];
     }
     // touched arbiters' cache entries at the positions reserved in merge order
-#pragma unroll
-    for (int k = 0; k < KREG; ++k) {
-      if (k < C.nc) {
-        const CSlot& c0 = C.reg[k];
-        const CSlot& c1 = k + 1 < KREG ? C.reg[k + 1 < KREG ? k + 1 : 0] : C.ovf[0];
-        write_arbiter_cache(S, W.par ^ 1, e, c0, c1);
-      }
+    static_for<0, KREG - 1>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      if (k < C.nc) write_arbiter_cache(S, W.par ^ 1, e, C.reg[k], C.reg[k + 1]);
+    });
+    if (KREG - 1 < C.nc) {
+      CSlot next = C.reg[KREG - 1];
+      if (KREG < C.nc) next = ovf[0];
+      write_arbiter_cache(S, W.par ^ 1, e, C.reg[KREG - 1], next);
     }
-    for (int k = KREG; k < C.nc; ++k) write_arbiter_cache(S, W.par ^ 1, e, C.ovf[k - KREG], C.ovf[k + 1 - KREG]);
+    for (int k = KREG; k < C.nc; ++k) write_arbiter_cache(S, W.par ^ 1, e, ovf[k - KREG], ovf[k + 1 - KREG]);
   }
+  STAMP(6);
   const int nn = W.out < MAXA ? W.out : MAXA;
   E.meta = (E.meta & ~((63u << 8) | META_PAR)) | ((uint32_t)nn << 8) | (W.par ? 0u : META_PAR);
 }
@@ -657,6 +765,7 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
                                                            int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
                                                            Counters* ctr) {
   __shared__ Lds L;
+  STAMP(0);
   const int lane = threadIdx.x;
   const int64_t e0 = (int64_t)blockIdx.x * MS_BLOCK;
   const int64_t e = e0 + lane;
@@ -682,8 +791,9 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
       active = false;
     }
   }
-  const uint64_t row_mask = __ballot(active);
+  stage_segments(P, L, lane);
   Env E;
+  Snap h2, h1;  // obs history snapshots t-2, t-1
   float pvx[5], pvy[5];
   bool fill3 = false, rng_dirty = false;
   if (active) {
@@ -709,8 +819,15 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
       tq[i] = F[2];
     }
     unsigned long long ovf = 0;
+    STAMP(1);
     physics_step(S, P, e, E, fx, fy, tq, L, lane, &ovf);
+    STAMP(7);
     if (ovf) atomicAdd(&ctr->overflow, ovf);
+    {  // history snapshots: issued here so their latency hides under the reward math
+      const int head = (E.meta & META_RING) ? 1 : 0;
+      snap_load(S, e, head ^ 1, h2);
+      snap_load(S, e, head, h1);
+    }
 
     // goal detection (game.py:401-412)
     int goal = 0;
@@ -742,26 +859,26 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
       fill3 = true;
     }
   }
-  __syncthreads();  // LDS physics scratch -> obs staging
-  emit_frames(S, P, e, E, active, fill3, obs, L, lane, row_mask, e0);
+  STAMP(8);
   if (active) {
+    emit_frames(S, P, e, E, fill3, h2, h1, obs);
+    STAMP(9);
     if (rng_dirty) store_rng(S, e, E);
     store_bodies(S, e, E);
     store_scalars(S, e, E);
   }
+  STAMP(10);
 }
 
 __global__ __launch_bounds__(MS_BLOCK) void ms_reset_kernel(DevState S, Params P, const uint64_t* __restrict__ pcg,
                                                             const uint8_t* __restrict__ mask, int mode, int set_hist_empty,
                                                             float* __restrict__ obs) {
-  __shared__ Lds L;
-  const int lane = threadIdx.x;
-  const int64_t e0 = (int64_t)blockIdx.x * MS_BLOCK;
-  const int64_t e = e0 + lane;
+  const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + threadIdx.x;
   const bool active = e < S.n && (!mask || mask[e]);
-  const uint64_t row_mask = __ballot(active);
+  if (!active) return;
   Env E;
-  if (active) {
+  Snap h0;  // unused: fill3 frames come from the fresh state
+  {
     load_scalars(S, e, E);
     if (pcg) {
       E.rng.shi = pcg[e * 4 + 0]; E.rng.slo = pcg[e * 4 + 1];
@@ -772,8 +889,8 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_reset_kernel(DevState S, Params P
     }
     reset_env_regs(E, mode);
   }
-  emit_frames(S, P, e, E, active, true, obs, L, lane, row_mask, e0);
-  if (active) {
+  emit_frames(S, P, e, E, true, h0, h0, obs);
+  {
     if (set_hist_empty) E.meta |= META_HE;
     store_rng(S, e, E);
     store_bodies(S, e, E);
@@ -812,11 +929,10 @@ __global__ void ms_export_kernel(DevState S, ms_env_state* __restrict__ out) {
     d.w = E.w[b]; d.vbx = E.vbx[b]; d.vby = E.vby[b]; d.wb = E.wb[b];
   }
   const int head = (E.meta & META_RING) ? 1 : 0;
-  for (int a = 0; a < 4; ++a)
-    for (int k = 0; k < 22; ++k) {
-      o.frames[0][a][k] = S.F[(int64_t)(F_HIST + (head ^ 1) * 88 + a * 22 + k) * n + e];
-      o.frames[1][a][k] = S.F[(int64_t)(F_HIST + head * 88 + a * 22 + k) * n + e];
-    }
+  for (int k = 0; k < MS_SNAP_SIZE; ++k) {
+    o.snap[0][k] = S.F[(int64_t)(F_SNAP + (head ^ 1) * MS_SNAP_SIZE + k) * n + e];
+    o.snap[1][k] = S.F[(int64_t)(F_SNAP + head * MS_SNAP_SIZE + k) * n + e];
+  }
   o.steps = E.steps; o.score_blue = E.score_blue; o.score_red = E.score_red;
   o.mode = (uint8_t)META_MODE(E.meta);
   o.hist_empty = (E.meta & META_HE) ? 1 : 0;
@@ -857,11 +973,10 @@ __global__ void ms_import_kernel(DevState S, const ms_env_state* __restrict__ in
   E.meta = (uint32_t)(o.mode & 3) | (o.hist_empty ? META_HE : 0u) | ((uint32_t)nc << 8) | (o.has_uint32 ? META_H32 : 0u);
   E.rng.shi = o.pcg_state_hi; E.rng.slo = o.pcg_state_lo; E.rng.ihi = o.pcg_inc_hi; E.rng.ilo = o.pcg_inc_lo;
   E.rng.has32 = o.has_uint32; E.rng.u32 = o.uinteger;
-  for (int a = 0; a < 4; ++a)
-    for (int k = 0; k < 22; ++k) {
-      S.F[(int64_t)(F_HIST + 0 * 88 + a * 22 + k) * n + e] = o.frames[0][a][k];  // ring head = 1
-      S.F[(int64_t)(F_HIST + 1 * 88 + a * 22 + k) * n + e] = o.frames[1][a][k];
-    }
+  for (int k = 0; k < MS_SNAP_SIZE; ++k) {  // ring head = 1
+    S.F[(int64_t)(F_SNAP + 0 * MS_SNAP_SIZE + k) * n + e] = o.snap[0][k];
+    S.F[(int64_t)(F_SNAP + 1 * MS_SNAP_SIZE + k) * n + e] = o.snap[1][k];
+  }
   E.meta |= META_RING;
   for (int k = 0; k < nc; ++k) {
     const ms_arbiter_state& A = o.arb[k];
@@ -1088,6 +1203,12 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
   h->S.CH = (uint32_t*)base; base += bytes_CH;
   h->S.CJ = (float*)base; base += bytes_CJ;
   h->S.n = n_envs;
+  h->S.stamps = nullptr;
+#ifdef MS_STAMPS
+  if (hipMalloc((void**)&h->S.stamps, sizeof(unsigned long long) * 16 * ((n + MS_BLOCK - 1) / MS_BLOCK)) != hipSuccess)
+    return fail(MS_ERR_OUT_OF_MEMORY, "stamps");
+  (void)hipMemsetAsync(h->S.stamps, 0, sizeof(unsigned long long) * 16 * ((n + MS_BLOCK - 1) / MS_BLOCK), h->stream);
+#endif
   if (hipMalloc((void**)&h->ctr, sizeof(Counters)) != hipSuccess) {
     (void)hipFree(h->mem);
     delete h;
@@ -1201,6 +1322,14 @@ int ms_get_stats(ms_env* h, ms_stats* out) {
   out->first_nonfinite_env = c.first_bad == (long long)INT64_MAX ? -1 : c.first_bad;
   return MS_OK;
 }
+
+#ifdef MS_STAMPS
+int ms_debug_stamps(ms_env* h, void** ptr, int64_t* n_waves) {
+  *ptr = h->S.stamps;
+  *n_waves = (h->n + MS_BLOCK - 1) / MS_BLOCK;
+  return MS_OK;
+}
+#endif
 
 int ms_reset_stats(ms_env* h) {
   if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_reset_stats: null handle");

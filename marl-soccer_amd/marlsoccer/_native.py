@@ -49,7 +49,7 @@ BODY_DTYPE = np.dtype([(n, "<f4") for n in ("px", "py", "vx", "vy", "angle", "w"
 ARB_DTYPE = np.dtype([("pair", "u1"), ("count", "u1"), ("idle", "u1"), ("pad0", "u1"),
                       ("hash", "u1", (2,)), ("pad1", "u1", (2,)), ("jn", "<f4", (2,)), ("jt", "<f4", (2,))])
 ENV_STATE_DTYPE = np.dtype([
-    ("body", BODY_DTYPE, (5,)), ("frames", "<f4", (2, 4, 22)),
+    ("body", BODY_DTYPE, (5,)), ("snap", "<f4", (2, 26)),
     ("steps", "<i4"), ("score_blue", "<i4"), ("score_red", "<i4"),
     ("mode", "u1"), ("hist_empty", "u1"), ("n_arb", "u1"), ("has_uint32", "u1"),
     ("uinteger", "<u4"), ("pad", "<u4"),

@@ -38,7 +38,7 @@ ARB_DTYPE = np.dtype([("pair", "u1"), ("count", "u1"), ("idle", "u1"), ("pad0", 
                       ("hash", "u1", (2,)), ("pad1", "u1", (2,)), ("jn", "<f4", (2,)), ("jt", "<f4", (2,))])
 MAX_ARB = 32
 ENV_STATE_DTYPE = np.dtype([
-    ("body", BODY_DTYPE, (5,)), ("frames", "<f4", (2, 4, 22)),
+    ("body", BODY_DTYPE, (5,)), ("snap", "<f4", (2, 26)),
     ("steps", "<i4"), ("score_blue", "<i4"), ("score_red", "<i4"),
     ("mode", "u1"), ("hist_empty", "u1"), ("n_arb", "u1"), ("has_uint32", "u1"),
     ("uinteger", "<u4"), ("pad", "<u4"),
@@ -96,6 +96,7 @@ def load(precision: str):
     lib.orc_batch_positions.argtypes = [P, C.c_int, P]
     lib.orc_batch_rng.argtypes = [P, C.c_int, P]
     lib.orc_batch_soft_reset.argtypes = [P, C.c_int]
+    lib.orc_batch_ncontacts.argtypes = [P, C.c_int, P]
     lib.orc_cpu_baseline.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_uint64]
     lib.orc_cpu_baseline.restype = C.c_double
     lib.orc_precision.restype = C.c_char_p
@@ -162,6 +163,11 @@ class OracleBatch:
 
     def soft_reset(self) -> None:
         self.lib.orc_batch_soft_reset(self.envs, self.n)
+
+    def ncontacts(self) -> np.ndarray:
+        out = np.zeros((self.n,), np.int32)
+        self.lib.orc_batch_ncontacts(self.envs, self.n, _ptr(out))
+        return out
 
     def overflow(self) -> int:
         return int(self.lib.orc_batch_overflow(self.envs, self.n))

@@ -795,11 +795,15 @@ static int rng_int4(orc_rng *g) { /* integers(0, 4): Lemire on 32 bits, rng_excl
 /* ------------------------------------------------------------------------------------ */
 /* Environment (Game + SoccerEnv + vec-env auto-reset)                                   */
 /* ------------------------------------------------------------------------------------ */
+/* obs history snapshot (include/marl_soccer.h MS_SNAP_SIZE): px[5], py[5], vx[4], vy[4],
+ * angle[4], w[4] — the whole input of Game._get_observations */
+typedef struct { real v[MS_SNAP_SIZE]; } orc_snap;
+
 typedef struct orc_env {
   orc_space sp;
   orc_rng rng;
   int steps, score_blue, score_red, mode, hist_empty;
-  float hist[2][4][22];
+  orc_snap hist[2]; /* [0] = t-2, [1] = t-1 */
 } orc_env;
 
 ORC_API int orc_sizeof_env(void) { return (int)sizeof(orc_env); }
@@ -864,23 +868,36 @@ static void vec_to_unit_mag(real dx, real dy, float *o) {
   o[2] = (float)(mag / (real)1000.0); /* field diagonal hypot(800, 600) */
 }
 
-ORC_API void orc_observe_space(const orc_space *sp, const orc_params *P, float frame[4][22]) {
+static void snapshot(const orc_space *sp, orc_snap *s) {
+  for (int b = 0; b < 5; ++b) { s->v[b] = sp->body[b].px; s->v[5 + b] = sp->body[b].py; }
+  for (int i = 0; i < 4; ++i) {
+    s->v[10 + i] = sp->body[i].vx; s->v[14 + i] = sp->body[i].vy;
+    s->v[18 + i] = sp->body[i].a; s->v[22 + i] = sp->body[i].w;
+  }
+}
+
+static void observe_snap(const orc_snap *sn, const orc_params *P, float frame[4][22]) {
   static const int TEAM[4] = {1, 0, 3, 2};
   static const int OPP[4][2] = {{2, 3}, {2, 3}, {0, 1}, {0, 1}};
-  const orc_body *b = sp->body;
+  const real *px = sn->v, *py = sn->v + 5, *vx = sn->v + 10, *vy = sn->v + 14, *an = sn->v + 18, *w = sn->v + 22;
   for (int i = 0; i < 4; ++i) {
     float *o = frame[i];
-    o[0] = (float)b[i].vx / (float)P->obs_vmax;
-    o[1] = (float)b[i].vy / (float)P->obs_vmax;
-    o[2] = (float)orc_angle_obs(b[i].a);
-    o[3] = (float)(b[i].w / P->obs_wmax);
+    o[0] = (float)vx[i] / (float)P->obs_vmax;
+    o[1] = (float)vy[i] / (float)P->obs_vmax;
+    o[2] = (float)orc_angle_obs(an[i]);
+    o[3] = (float)(w[i] / P->obs_wmax);
     const int others[4] = {TEAM[i], OPP[i][0], OPP[i][1], 4};
-    for (int k = 0; k < 4; ++k)
-      vec_to_unit_mag(b[others[k]].px - b[i].px, b[others[k]].py - b[i].py, o + 4 + 3 * k);
+    for (int k = 0; k < 4; ++k) vec_to_unit_mag(px[others[k]] - px[i], py[others[k]] - py[i], o + 4 + 3 * k);
     real own_x = i < 2 ? (real)10 : (real)790, opp_x = i < 2 ? (real)790 : (real)10;
-    vec_to_unit_mag(own_x - b[i].px, (real)300 - b[i].py, o + 16);
-    vec_to_unit_mag(opp_x - b[i].px, (real)300 - b[i].py, o + 19);
+    vec_to_unit_mag(own_x - px[i], (real)300 - py[i], o + 16);
+    vec_to_unit_mag(opp_x - px[i], (real)300 - py[i], o + 19);
   }
+}
+
+ORC_API void orc_observe_space(const orc_space *sp, const orc_params *P, float frame[4][22]) {
+  orc_snap s;
+  snapshot(sp, &s);
+  observe_snap(&s, P, frame);
 }
 
 /* prev_d - cur_d for d = |a - b| (game.py:336-338, 344-345), restated as
@@ -942,7 +959,8 @@ ORC_API void orc_env_reset(orc_env *e, const orc_params *P, const uint64_t *pcg,
   spawn(e, mode);
   float f[4][22];
   orc_observe_space(&e->sp, P, f);
-  memcpy(e->hist[0], f, sizeof(f)); memcpy(e->hist[1], f, sizeof(f));
+  snapshot(&e->sp, &e->hist[0]);
+  e->hist[1] = e->hist[0];
   e->hist_empty = 0;
   if (obs)
     for (int i = 0; i < 4; ++i)
@@ -990,17 +1008,21 @@ ORC_API int orc_env_step(orc_env *e, const orc_params *P, const float *act, floa
   if (goal) spawn(e, e->mode);
   if (done) r = blue_reward(P, prev, cur, goal, 1, e->score_blue, e->score_red);
 
-  float f[4][22];
-  orc_observe_space(&e->sp, P, f);
-  if (e->hist_empty) { memcpy(e->hist[0], f, sizeof(f)); memcpy(e->hist[1], f, sizeof(f)); e->hist_empty = 0; }
+  orc_snap now;
+  snapshot(&e->sp, &now);
+  if (e->hist_empty) { e->hist[0] = now; e->hist[1] = now; e->hist_empty = 0; }
+  float f0[4][22], f1[4][22], f[4][22];
+  observe_snap(&e->hist[0], P, f0);
+  observe_snap(&e->hist[1], P, f1);
+  observe_snap(&now, P, f);
   if (obs)
     for (int i = 0; i < 4; ++i) {
-      memcpy(obs + i * 66, e->hist[0][i], 22 * sizeof(float));
-      memcpy(obs + i * 66 + 22, e->hist[1][i], 22 * sizeof(float));
+      memcpy(obs + i * 66, f0[i], 22 * sizeof(float));
+      memcpy(obs + i * 66 + 22, f1[i], 22 * sizeof(float));
       memcpy(obs + i * 66 + 44, f[i], 22 * sizeof(float));
     }
-  memcpy(e->hist[0], e->hist[1], sizeof(f));
-  memcpy(e->hist[1], f, sizeof(f));
+  e->hist[0] = e->hist[1];
+  e->hist[1] = now;
   if (rew) { rew[0] = (double)r; rew[1] = (double)r; rew[2] = 0.0; rew[3] = 0.0; }
   if (trunc) for (int i = 0; i < 4; ++i) trunc[i] = (uint8_t)done;
   if (goal_out) *goal_out = (int8_t)goal;
@@ -1023,7 +1045,8 @@ ORC_API void orc_env_export(const orc_env *e, ms_env_state *s) {
     d->angle = b < 4 ? (float)o->a : 0.0f; d->w = (float)o->w;
     d->vbx = (float)o->vbx; d->vby = (float)o->vby; d->wb = (float)o->wb;
   }
-  memcpy(s->frames, e->hist, sizeof(s->frames));
+  for (int k = 0; k < 2; ++k)
+    for (int j = 0; j < MS_SNAP_SIZE; ++j) s->snap[k][j] = (float)e->hist[k].v[j];
   s->steps = e->steps; s->score_blue = e->score_blue; s->score_red = e->score_red;
   s->mode = (uint8_t)e->mode; s->hist_empty = (uint8_t)e->hist_empty;
   s->has_uint32 = (uint8_t)e->rng.has_uint32; s->uinteger = e->rng.uinteger;
@@ -1046,7 +1069,8 @@ ORC_API void orc_env_import(orc_env *e, const ms_env_state *s) {
     o->px = d->px; o->py = d->py; o->vx = d->vx; o->vy = d->vy; o->a = b < 4 ? d->angle : 0;
     o->w = d->w; o->vbx = d->vbx; o->vby = d->vby; o->wb = d->wb;
   }
-  memcpy(e->hist, s->frames, sizeof(e->hist));
+  for (int k = 0; k < 2; ++k)
+    for (int j = 0; j < MS_SNAP_SIZE; ++j) e->hist[k].v[j] = s->snap[k][j];
   e->steps = s->steps; e->score_blue = s->score_blue; e->score_red = s->score_red;
   e->mode = s->mode; e->hist_empty = s->hist_empty;
   e->rng.has_uint32 = s->has_uint32; e->rng.uinteger = s->uinteger;
@@ -1109,6 +1133,14 @@ ORC_API void orc_batch_rng(const orc_env *envs, int n, uint64_t *out) {
 }
 ORC_API void orc_batch_soft_reset(orc_env *envs, int n) {
   for (int i = 0; i < n; ++i) orc_env_soft_reset(&envs[i]);
+}
+/* contacts in each env's last physics step (instrumentation for kernel tuning) */
+ORC_API void orc_batch_ncontacts(const orc_env *envs, int n, int32_t *out) {
+  for (int i = 0; i < n; ++i) {
+    int c = 0;
+    for (int k = 0; k < envs[i].sp.n_arb; ++k) c += envs[i].sp.arb[k].count;
+    out[i] = c;
+  }
 }
 ORC_API unsigned long long orc_batch_overflow(const orc_env *envs, int n) {
   unsigned long long s = 0;

@@ -122,7 +122,11 @@ def dribble(env, obs, agent, target_goal, steps):
         goal = vec_from(f, target_goal)
         g_dir = (goal - ball) / (np.linalg.norm(goal - ball) + 1e-9)
         behind = ball - 24.0 * g_dir
-        if np.linalg.norm(behind) < 6.0 or (np.dot(ball, g_dir) > 0 and np.linalg.norm(ball) < 30):
+        if float(np.dot(-ball, g_dir)) > -12.0:  # not behind the ball: go round it on our side
+            perp = np.array([-g_dir[1], g_dir[0]])
+            side = 1.0 if np.dot(-ball, perp) >= 0 else -1.0
+            move = ball - 30.0 * g_dir + side * 45.0 * perp
+        elif np.linalg.norm(behind) < 6.0 or np.linalg.norm(ball) < 30:
             move = ball + 20.0 * g_dir
         else:
             move = behind

@@ -79,4 +79,4 @@ def test_state_record_layout_matches_oracle():
     import oracle as orc
     from marlsoccer import _native as N
     assert N.ENV_STATE_DTYPE == orc.ENV_STATE_DTYPE
-    assert N.ENV_STATE_DTYPE.itemsize == 1712
+    assert N.ENV_STATE_DTYPE.itemsize == 1216

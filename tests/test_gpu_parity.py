@@ -49,7 +49,7 @@ def assert_state_equal(gpu_st, orc_st, where=""):
         np.testing.assert_array_equal(gpu_st[f], orc_st[f], err_msg=f"{where} {f}")
     for f in ("px", "py", "vx", "vy", "angle", "w", "vbx", "vby", "wb"):
         np.testing.assert_array_equal(gpu_st["body"][f], orc_st["body"][f], err_msg=f"{where} body.{f}")
-    np.testing.assert_array_equal(gpu_st["frames"], orc_st["frames"], err_msg=f"{where} frames")
+    np.testing.assert_array_equal(gpu_st["snap"], orc_st["snap"], err_msg=f"{where} snap")
     for i in range(len(gpu_st)):
         k = int(orc_st["n_arb"][i])
         for f in ("pair", "count", "idle", "hash", "jn", "jt"):
