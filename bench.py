@@ -8,8 +8,11 @@
 One "step" = one env.step of every env resident on a GPU (one ms_step launch): E envs per
 GPU (default 65,536 = BASELINE.json configs[2]), weak scaling across ranks (envs are
 independent; no collective in the data path). Actions are synthetic uniform(-1, 1) fp32
-generated on the device before the timed region and read from HBM every step. Rank 0
-prints ONE JSON line. --allgather adds the optional RCCL all-gather of obs (configs[3]).
+from torch's device Philox generator, one fresh (E, 4, 3) buffer per step (generated
+before the timed region, read from HBM every step). The default timed
+window is one whole episode (max_steps = 1000, including the synchronised auto-reset),
+so contact-heavy and contact-free phases are both in the average. Rank 0 prints ONE JSON
+line. --allgather adds the optional RCCL all-gather of obs (configs[3]).
 """
 from __future__ import annotations
 
@@ -34,14 +37,16 @@ ARB_BYTES = 20                       # one cached arbiter: header + 4 impulses (
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
-    ap.add_argument("--action-sets", type=int, default=64, help="distinct device action buffers cycled")
+    ap.add_argument("--action-sets", type=int, default=0,
+                    help="distinct device action buffers cycled (0: one per step, capped at --action-gib)")
+    ap.add_argument("--action-gib", type=float, default=8.0, help="HBM cap for the action pool")
     ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of obs after every step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-envs", type=int, default=16384)
-    ap.add_argument("--cpu-steps", type=int, default=1500)
+    ap.add_argument("--cpu-envs", type=int, default=65536)
+    ap.add_argument("--cpu-steps", type=int, default=3000)
     return ap.parse_args()
 
 
@@ -92,7 +97,9 @@ def main():
     batch.reset(seed=19 + rank * E)  # env i of rank r seeded 19 + r*E + i (global index)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
-    nsets = max(1, min(args.action_sets, args.steps + args.warmup))
+    want = args.action_sets if args.action_sets > 0 else args.steps + args.warmup
+    cap = max(1, int(args.action_gib * (1 << 30) // (E * 48)))
+    nsets = max(1, min(want, cap, args.steps + args.warmup))
     actions = [torch.rand((E, 4, 3), device=dev, generator=gen) * 2 - 1 for _ in range(nsets)]
     obs, rew = batch.obs, batch.rew
     term, trunc, goal, score = batch.term, batch.trunc, batch.goal, batch.score
@@ -162,15 +169,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: uniform(-1,1) fp32 actions (device Philox, read from HBM each step); "
-                    "env i seeded 19+i; default config.json physics/rewards",
+            "data": f"synthetic: uniform(-1,1) fp32 actions (device Philox, {nsets} distinct (E,4,3) buffers "
+                    f"for {args.warmup + args.steps} steps, read from HBM each step); env i seeded 19+i; "
+                    "default config.json physics/rewards",
             "config": {"workload": f"{E} parallel envs per MI355X (BASELINE.json configs[2])",
                        "envs_per_gpu": E, "global_envs": world * E, "max_steps": 1000,
                        "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "ms_step_kernel", "kernel_ms": kern_ms,
-                         "alg_bytes_per_env_step": bytes_per_step, "mean_cached_arbiters": mean_arb,
+                         "alg_bytes_per_env_step": bytes_per_step,
+                         "mean_cached_arbiters": mean_arb,  # sampled after the timed window
                          "pmc": pmc_info},
             "arbiter_overflow": stats["arbiter_overflow"],
         }

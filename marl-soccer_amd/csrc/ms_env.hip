@@ -62,6 +62,7 @@ struct DevState {
   uint64_t* R;
   uint32_t* CH;
   float* CJ;
+  void* SP;  // contact slots KREG.. of each env (pile-ups only): [env][MAXC - KREG] CSlot
   int64_t n;
 };
 
@@ -152,6 +153,16 @@ struct Lds {
   } ph;
 };
 
+// Compile-time loop: every reg[] access below uses a constant index from the first IR on,
+// so the slots are promoted to registers (an unrolled runtime loop is not: SROA runs first).
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
 // ---- frames -----------------------------------------------------------------------------
 __device__ __forceinline__ void frame_of(const Params& P, const Env& E, int agent, float* o) {
   switch (agent) {
@@ -192,46 +203,61 @@ __device__ __forceinline__ void snap_store(const DevState& S, int64_t e, int slo
     p[(int64_t)(18 + i) * S.n] = s.ang[i]; p[(int64_t)(22 + i) * S.n] = s.w[i];
   }
 }
-template <int A>
-__device__ __forceinline__ void snap_frame(const Params& P, const Snap& s, float* o) {
-  agent_frame<A>(P, s.px, s.py, s.vx, s.vy, s.ang, s.w, o);
-}
-
-// One 22-float frame of the 528-B block of an agent pair (soccer_env.py:130-140 stacks
-// [t-2, t-1, t] per agent). Frame K (0..5) = agent 2*PAIR + K/3, snapshot K%3. Frames start
-// 88 B apart, so even frames are 16-B aligned: five float4 stores plus a 2-float carry that
-// the next (odd) frame completes, i.e. 33 float4 stores per pair with 24 live floats.
-template <int PAIR, int K>
-__device__ __forceinline__ void store_obs_frame(const Params& P, const Snap& s2, const Snap& s1, const Snap& s0,
-                                                float4* __restrict__ d, float& c0, float& c1) {
-  constexpr int A = 2 * PAIR + K / 3;
-  const Snap& s = (K % 3 == 0) ? s2 : ((K % 3 == 1) ? s1 : s0);
-  float f[22];
-  snap_frame<A>(P, s, f);
-  if constexpr ((K & 1) == 0) {
-    const int q0 = (22 * K) / 4;
+// 22 floats at a 8-B aligned address: five 16-B stores and one 8-B store, the 8-B one first
+// when the frame starts half-way into a 16-B word
+template <bool ALIGNED16>
+__device__ __forceinline__ void store_frame22(float* __restrict__ d, const float* f) {
+  if constexpr (ALIGNED16) {
 #pragma unroll
-    for (int q = 0; q < 5; ++q) d[q0 + q] = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
-    c0 = f[20]; c1 = f[21];
+    for (int q = 0; q < 5; ++q) *(float4*)(d + 4 * q) = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
+    *(float2*)(d + 20) = make_float2(f[20], f[21]);
   } else {
-    const int q0 = (22 * K - 2) / 4;
-    d[q0] = make_float4(c0, c1, f[0], f[1]);
+    *(float2*)d = make_float2(f[0], f[1]);
 #pragma unroll
-    for (int q = 0; q < 5; ++q) d[q0 + 1 + q] = make_float4(f[2 + 4 * q], f[3 + 4 * q], f[4 + 4 * q], f[5 + 4 * q]);
+    for (int q = 0; q < 5; ++q)
+      *(float4*)(d + 2 + 4 * q) = make_float4(f[2 + 4 * q], f[3 + 4 * q], f[4 + 4 * q], f[5 + 4 * q]);
   }
 }
 
-template <int PAIR>
-__device__ __forceinline__ void store_obs_pair(const Params& P, const Snap& s2, const Snap& s1, const Snap& s0,
-                                               float* __restrict__ dst) {
-  float4* d = (float4*)dst;
-  float c0, c1;
-  store_obs_frame<PAIR, 0>(P, s2, s1, s0, d, c0, c1);
-  store_obs_frame<PAIR, 1>(P, s2, s1, s0, d, c0, c1);
-  store_obs_frame<PAIR, 2>(P, s2, s1, s0, d, c0, c1);
-  store_obs_frame<PAIR, 3>(P, s2, s1, s0, d, c0, c1);
-  store_obs_frame<PAIR, 4>(P, s2, s1, s0, d, c0, c1);
-  store_obs_frame<PAIR, 5>(P, s2, s1, s0, d, c0, c1);
+// The four agents' frames of one snapshot (Game._get_observations, game.py:258-322), stored
+// as stacked-frame slot K (0 = t-2, 1 = t-1, 2 = t; soccer_env.py:130-140) of every agent's
+// 66-float row. The six agent-agent vectors are computed once per pair: agent j's vector to
+// agent i is the exact negation of i's to j (IEEE a-b = -(b-a), same magnitude), written as
+// 0 - u so that a zero component stays +0 as the direct evaluation gives.
+template <int K>
+__device__ __forceinline__ void emit_snapshot(const Params& P, const Snap& s, float* __restrict__ row0) {
+  constexpr int PI_[6] = {0, 0, 0, 1, 1, 2}, PJ_[6] = {1, 2, 3, 2, 3, 3};
+  float aa[6][3];
+#pragma unroll
+  for (int p = 0; p < 6; ++p) unit_mag(s.px[PJ_[p]] - s.px[PI_[p]], s.py[PJ_[p]] - s.py[PI_[p]], aa[p]);
+  static_for<0, 4>([&](auto ac) __attribute__((always_inline)) {
+    constexpr int A = decltype(ac)::value;
+    // obs slots 4 (teammate), 7, 10 (opponents in index order) -> (pair, mirrored)
+    constexpr int TEAM = A ^ 1, O1 = A < 2 ? 2 : 0, O2 = A < 2 ? 3 : 1;
+    constexpr int OTH[3] = {TEAM, O1, O2};
+    float f[22];
+    f[0] = s.vx[A] / P.obs_vmax;
+    f[1] = s.vy[A] / P.obs_vmax;
+    f[2] = angle_obs(s.ang[A]);
+    f[3] = s.w[A] / P.obs_wmax;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int B = OTH[k];
+      const int lo = A < B ? A : B, hi = A < B ? B : A;
+      const int p = lo == 0 ? hi - 1 : (lo == 1 ? hi + 1 : 5);
+      if (A < B) {
+        f[4 + 3 * k] = aa[p][0]; f[5 + 3 * k] = aa[p][1];
+      } else {
+        f[4 + 3 * k] = 0.0f - aa[p][0]; f[5 + 3 * k] = 0.0f - aa[p][1];
+      }
+      f[6 + 3 * k] = aa[p][2];
+    }
+    unit_mag(s.px[4] - s.px[A], s.py[4] - s.py[A], f + 13);
+    const float own_x = A < 2 ? 10.0f : 790.0f, opp_x = A < 2 ? 790.0f : 10.0f;
+    unit_mag(own_x - s.px[A], 300.0f - s.py[A], f + 16);
+    unit_mag(opp_x - s.px[A], 300.0f - s.py[A], f + 19);
+    store_frame22<((A + K) & 1) == 0>(row0 + A * 66 + K * 22, f);
+  });
 }
 
 // Obs output + history ring update. fill3: all three frames are the current one (reset,
@@ -246,8 +272,9 @@ __device__ __forceinline__ void emit_frames(const DevState& S, const Params& P, 
   const Snap& s1 = fill3 ? s0 : s1_in;
   if (obs && MS_ABLATE != 3) {
     float* dst = obs + e * 264;
-    store_obs_pair<0>(P, s2, s1, s0, dst);
-    store_obs_pair<1>(P, s2, s1, s0, dst + 132);
+    emit_snapshot<0>(P, s2, dst);
+    emit_snapshot<1>(P, s1, dst);
+    emit_snapshot<2>(P, s0, dst);
   }
   if (fill3) {
     snap_store(S, e, 0, s0);
@@ -288,9 +315,16 @@ __device__ __forceinline__ void soft_reset_regs(Env& E) {
 // copy the segment table from the kernel arguments with constant indices (a per-lane index
 // into the by-value Params would make the compiler copy all of Params to scratch)
 __device__ __forceinline__ void stage_segments(const Params& P, Lds& L, int lane) {
+  // field by field: a whole-struct copy becomes a memcpy out of a private copy of Params
+  // (scratch stores in every lane)
   if (lane == 0) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) L.seg[s] = P.seg[s];
+    for (int s = 0; s < 8; ++s) {
+      L.seg[s].ax = P.seg[s].ax; L.seg[s].ay = P.seg[s].ay; L.seg[s].bx = P.seg[s].bx; L.seg[s].by = P.seg[s].by;
+      L.seg[s].nx = P.seg[s].nx; L.seg[s].ny = P.seg[s].ny; L.seg[s].r = P.seg[s].r;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) L.seg[s].bb[k] = P.seg[s].bb[k];
+    }
   }
   __syncthreads();
 }
@@ -311,7 +345,9 @@ struct CSlot {
 #define CS_POS(m) ((int)(((m) >> 18) & 63u))
 #define CS_PAIR(m) ((int)(((m) >> 24) & 63u))
 
-#define KREG 8                          // contacts held in registers
+#ifndef KREG
+#define KREG 8  // contacts held in registers; further ones go to the global spill (pile-ups)
+#endif
 #define MAXC (2 * MAXA)                 // contact capacity (2 per arbiter)
 
 __device__ __forceinline__ float cache_field(const DevState& S, int par, int k, int f, int64_t e) {
@@ -332,16 +368,6 @@ struct Contacts {
   int nc, na;
 };
 
-// Compile-time loop: every reg[] access below uses a constant index from the first IR on,
-// so the slots are promoted to registers (an unrolled runtime loop is not: SROA runs first).
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
 // d = c ? s : d, field by field with unconditional stores: a conditional whole-struct store
 // lets the optimizer merge the KREG stores into one store through a phi of slot pointers,
 // which pins the slots in scratch memory.
@@ -353,7 +379,7 @@ __device__ __forceinline__ void slot_select(CSlot& d, const CSlot& s, bool c) {
   d.m = c ? s.m : d.m;
 }
 
-// overflow slots KREG..MAXC-1 live in private memory; only pile-ups reach them
+// overflow slots KREG..MAXC-1 live in the global spill buffer; only pile-ups reach them
 __device__ __forceinline__ void slot_put(Contacts& C, CSlot* ovf, int k, const CSlot& s) {
   static_for<0, KREG>([&](auto qc) __attribute__((always_inline)) {
     constexpr int q = decltype(qc)::value;
@@ -623,7 +649,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
   mAA = mBA = mSA = mBS = 0;
 #endif
 
-  CSlot ovf[MAXC - KREG];
+  CSlot* ovf = (CSlot*)S.SP + e * (MAXC - KREG);
   Contacts C;
   C.nc = 0;
   C.na = 0;
@@ -1204,6 +1230,13 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
   h->S.CJ = (float*)base; base += bytes_CJ;
   h->S.n = n_envs;
   h->S.stamps = nullptr;
+  // contact-slot spill for pile-ups beyond KREG contacts: reserved address space, touched
+  // only by envs with more than KREG contacts (no traffic in ordinary play)
+  if (hipMalloc(&h->S.SP, sizeof(CSlot) * (MAXC - KREG) * n) != hipSuccess) {
+    (void)hipFree(h->mem);
+    delete h;
+    return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of the contact spill buffer failed");
+  }
 #ifdef MS_STAMPS
   if (hipMalloc((void**)&h->S.stamps, sizeof(unsigned long long) * 16 * ((n + MS_BLOCK - 1) / MS_BLOCK)) != hipSuccess)
     return fail(MS_ERR_OUT_OF_MEMORY, "stamps");
@@ -1211,6 +1244,7 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
 #endif
   if (hipMalloc((void**)&h->ctr, sizeof(Counters)) != hipSuccess) {
     (void)hipFree(h->mem);
+    (void)hipFree(h->S.SP);
     delete h;
     return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of counters failed");
   }
@@ -1245,6 +1279,7 @@ int ms_destroy(ms_env* h) {
   (void)hipSetDevice(h->device);
   (void)hipStreamSynchronize(h->stream);
   (void)hipFree(h->mem);
+  (void)hipFree(h->S.SP);
   (void)hipFree(h->ctr);
   delete h;
   return MS_OK;
