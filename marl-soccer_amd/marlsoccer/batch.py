@@ -207,3 +207,8 @@ class SoccerBatch:
 
     def synchronize(self) -> None:
         self.stream.synchronize()
+
+    def set_stream(self, stream: torch.cuda.Stream) -> None:
+        """Launch subsequent calls on `stream` (e.g. a graph-capture stream; ms_set_stream)."""
+        N.check(self._L.ms_set_stream(self._h, C.c_void_p(stream.cuda_stream)), "ms_set_stream")
+        self.stream = stream
