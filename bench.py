@@ -84,10 +84,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MS_BENCH_SHARED_GPU=1 (rehearsal on a one-GPU box only): every rank on cuda:0, gloo for
+    # the barrier and the max-reduce; the driver's multi-GPU runs use one GPU per rank + RCCL
+    shared = os.environ.get("MS_BENCH_SHARED_GPU") == "1"
+    ordinal = 0 if shared else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(ordinal)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", ordinal))
+    dev = torch.device("cuda", ordinal if world > 1 else 0)
     torch.cuda.set_device(dev)
 
     from marlsoccer import SoccerBatch
@@ -138,7 +145,7 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
 
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if shared else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
@@ -172,7 +179,9 @@ def main():
             "data": f"synthetic: uniform(-1,1) fp32 actions (device Philox, {nsets} distinct (E,4,3) buffers "
                     f"for {args.warmup + args.steps} steps, read from HBM each step); env i seeded 19+i; "
                     "default config.json physics/rewards",
-            "config": {"workload": f"{E} parallel envs per MI355X (BASELINE.json configs[2])",
+            "config": {"workload": f"{E} parallel envs per MI355X" +
+                                   (" (BASELINE.json configs[2])" if E == 65536 else
+                                    " (BASELINE.json configs[1])" if E == 4096 else ""),
                        "envs_per_gpu": E, "global_envs": world * E, "max_steps": 1000,
                        "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
