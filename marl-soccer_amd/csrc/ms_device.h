@@ -30,6 +30,7 @@ struct Params {
   float e_aa, u_aa, e_ab, u_ab, e_aw, u_aw, e_ag, u_ag, e_bw, u_bw;
   float prox_mult, goal_mult, alive, goal_reward, concede_penalty, score_diff_mult;
   int max_steps, autoreset;
+  int fast_div;  // obs_vmax, obs_wmax inside div_nr's divisor domain (host-checked)
   Seg seg[8];
 };
 
@@ -93,9 +94,44 @@ __device__ __forceinline__ void sincos_contract(float x, float* s_out, float* c_
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Reduced-range IEEE division and square root. The compiler's correctly rounded fp32 division
+// is v_div_scale x2, v_rcp, Newton refinement, v_div_fmas, v_div_fixup; for a positive normal
+// divisor d in [2^-26, 2^13] and a numerator n = 0 or 2^-100 <= |n| <= 2^30, div_scale scales
+// nothing, div_fmas is a plain fma and div_fixup is the identity, so the sequence below returns
+// the same bits as n / d (and the reciprocal refinement is shared by every division by d).
+// Likewise sqrt_nr is the compiler's sqrtf without the tiny-input rescale and the zero/inf
+// class fix-up, identical for x in [2^-90, 2^126]. Both were checked on the MI355X against
+// IEEE over 1.7e10 random operands of those domains with no difference; callers guard their
+// inputs (frame_inputs_in_range) and take the IEEE path otherwise.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float rcp_nr(float d) {
+  const float r = __builtin_amdgcn_rcpf(d);
+  const float e = __builtin_fmaf(-d, r, 1.0f);
+  return __builtin_fmaf(e, r, r);
+}
+__device__ __forceinline__ float div_nr(float n, float d, float r) {
+  float q = n * r;
+  float e = __builtin_fmaf(-d, q, n);
+  q = __builtin_fmaf(e, r, q);
+  e = __builtin_fmaf(-d, q, n);
+  const float res = __builtin_fmaf(e, r, q);
+  return n == 0.0f ? n : res;  // keeps the sign of a zero numerator
+}
+__device__ __forceinline__ float sqrt_nr(float x) {
+  float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+  s = rm <= 0.0f ? sm : s;
+  s = rp > 0.0f ? sp : s;
+  return s;
+}
+
+template <bool FAST = false>
 __device__ __forceinline__ float angle_obs(float a) {
   float k = rintf(a * 0.15915493667125702f);
   float w = (a - k * 6.28125f) - k * 0.0019353071693331003f;
+  if constexpr (FAST) return div_nr(w, 3.1415927410125732f, rcp_nr(3.1415927410125732f));
   return w / 3.1415927410125732f;
 }
 
@@ -466,7 +502,18 @@ __device__ __forceinline__ void spawn_positions(Rng& g, int mode, float px[5], f
 // ------------------------------------------------------------------------------------------
 // Observations: Game._get_observations (game.py:258-322) -> fp32 (soccer_env.py:131)
 // ------------------------------------------------------------------------------------------
+template <bool FAST = false>
 __device__ __forceinline__ void unit_mag(float dx, float dy, float* o) {
+  if constexpr (FAST) {
+    float mag = sqrt_nr(dx * dx + dy * dy);
+    const float r = rcp_nr(mag);
+    const bool big = mag > 1e-8f;
+    o[0] = big ? div_nr(dx, mag, r) : 0.0f;
+    o[1] = big ? div_nr(dy, mag, r) : 0.0f;
+    mag = big ? mag : 0.0f;
+    o[2] = div_nr(mag, 1000.0f, rcp_nr(1000.0f));
+    return;
+  }
   float mag = sqrtf(dx * dx + dy * dy);
   if (mag > 1e-8f) {
     o[0] = dx / mag;

@@ -224,22 +224,28 @@ __device__ __forceinline__ void store_frame22(float* __restrict__ d, const float
 // 66-float row. The six agent-agent vectors are computed once per pair: agent j's vector to
 // agent i is the exact negation of i's to j (IEEE a-b = -(b-a), same magnitude), written as
 // 0 - u so that a zero component stays +0 as the direct evaluation gives.
-template <int K>
-__device__ __forceinline__ void emit_snapshot(const Params& P, const Snap& s, float* __restrict__ row0) {
+template <bool FAST, int K>
+__device__ __forceinline__ void emit_snapshot_impl(const Params& P, const Snap& s, float* __restrict__ row0) {
   constexpr int PI_[6] = {0, 0, 0, 1, 1, 2}, PJ_[6] = {1, 2, 3, 2, 3, 3};
   float aa[6][3];
 #pragma unroll
-  for (int p = 0; p < 6; ++p) unit_mag(s.px[PJ_[p]] - s.px[PI_[p]], s.py[PJ_[p]] - s.py[PI_[p]], aa[p]);
+  for (int p = 0; p < 6; ++p) unit_mag<FAST>(s.px[PJ_[p]] - s.px[PI_[p]], s.py[PJ_[p]] - s.py[PI_[p]], aa[p]);
   static_for<0, 4>([&](auto ac) __attribute__((always_inline)) {
     constexpr int A = decltype(ac)::value;
     // obs slots 4 (teammate), 7, 10 (opponents in index order) -> (pair, mirrored)
     constexpr int TEAM = A ^ 1, O1 = A < 2 ? 2 : 0, O2 = A < 2 ? 3 : 1;
     constexpr int OTH[3] = {TEAM, O1, O2};
     float f[22];
-    f[0] = s.vx[A] / P.obs_vmax;
-    f[1] = s.vy[A] / P.obs_vmax;
-    f[2] = angle_obs(s.ang[A]);
-    f[3] = s.w[A] / P.obs_wmax;
+    if constexpr (FAST) {
+      f[0] = div_nr(s.vx[A], P.obs_vmax, rcp_nr(P.obs_vmax));
+      f[1] = div_nr(s.vy[A], P.obs_vmax, rcp_nr(P.obs_vmax));
+      f[3] = div_nr(s.w[A], P.obs_wmax, rcp_nr(P.obs_wmax));
+    } else {
+      f[0] = s.vx[A] / P.obs_vmax;
+      f[1] = s.vy[A] / P.obs_vmax;
+      f[3] = s.w[A] / P.obs_wmax;
+    }
+    f[2] = angle_obs<FAST>(s.ang[A]);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int B = OTH[k];
@@ -252,12 +258,40 @@ __device__ __forceinline__ void emit_snapshot(const Params& P, const Snap& s, fl
       }
       f[6 + 3 * k] = aa[p][2];
     }
-    unit_mag(s.px[4] - s.px[A], s.py[4] - s.py[A], f + 13);
+    unit_mag<FAST>(s.px[4] - s.px[A], s.py[4] - s.py[A], f + 13);
     const float own_x = A < 2 ? 10.0f : 790.0f, opp_x = A < 2 ? 790.0f : 10.0f;
-    unit_mag(own_x - s.px[A], 300.0f - s.py[A], f + 16);
-    unit_mag(opp_x - s.px[A], 300.0f - s.py[A], f + 19);
+    unit_mag<FAST>(own_x - s.px[A], 300.0f - s.py[A], f + 16);
+    unit_mag<FAST>(opp_x - s.px[A], 300.0f - s.py[A], f + 19);
     store_frame22<((A + K) & 1) == 0>(row0 + A * 66 + K * 22, f);
   });
+}
+
+// Operands of a snapshot's frames inside the domains of div_nr / sqrt_nr (ms_device.h):
+// positions 0 or 2^-70..2^28 (so every difference is 0 or 2^-93..2^29), velocities, spins and
+// angles 0 or 2^-100..2^30. Two max/min reductions over the raw magnitudes (0 maps to ~0u).
+__device__ __forceinline__ bool frame_inputs_in_range(const Params& P, const Snap& s) {
+  uint32_t pmax = 0u, pmin = ~0u, vmax = 0u, vmin = ~0u;
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    const uint32_t x = __float_as_uint(s.px[b]) & 0x7fffffffu, y = __float_as_uint(s.py[b]) & 0x7fffffffu;
+    pmax = max(pmax, max(x, y));
+    pmin = min(pmin, min(x - 1u, y - 1u));
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t a = __float_as_uint(s.vx[i]) & 0x7fffffffu, b = __float_as_uint(s.vy[i]) & 0x7fffffffu;
+    const uint32_t c = __float_as_uint(s.w[i]) & 0x7fffffffu, d = __float_as_uint(s.ang[i]) & 0x7fffffffu;
+    vmax = max(vmax, max(max(a, b), max(c, d)));
+    vmin = min(vmin, min(min(a - 1u, b - 1u), min(c - 1u, d - 1u)));
+  }
+  return P.fast_div && pmax <= 0x4D800000u && pmin >= 0x1C800000u - 1u && vmax <= 0x4E800000u &&
+         vmin >= 0x0D800000u - 1u;
+}
+
+template <int K>
+__device__ __forceinline__ void emit_snapshot(const Params& P, const Snap& s, float* __restrict__ row0) {
+  if (frame_inputs_in_range(P, s)) emit_snapshot_impl<true, K>(P, s, row0);
+  else emit_snapshot_impl<false, K>(P, s, row0);
 }
 
 // Obs output + history ring update. fill3: all three frames are the current one (reset,
@@ -1160,6 +1194,8 @@ static void make_params(const ms_config* cfg, Params* P) {
   P->torque_max = (float)cfg->action_torque_max;
   P->obs_vmax = (float)(cfg->max_velocity > 1e-6 ? cfg->max_velocity : 1e-6);
   P->obs_wmax = (float)(cfg->max_angular_velocity > 1e-6 ? cfg->max_angular_velocity : 1e-6);
+  P->fast_div = (P->obs_vmax >= 0x1p-20f && P->obs_vmax <= 0x1p12f && P->obs_wmax >= 0x1p-20f &&
+                 P->obs_wmax <= 0x1p12f) ? 1 : 0;
   const float ea = (float)cfg->agent_elasticity, ua = (float)cfg->agent_surface_friction;
   const float eb = (float)cfg->ball_elasticity, ub = (float)cfg->ball_surface_friction;
   const float ew = 0.95f, uw = 0.2f, eg = 0.95f, ug = 0.0f;
