@@ -855,7 +855,7 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
   Env E;
   Snap h2, h1;  // obs history snapshots t-2, t-1
   float pvx[5], pvy[5];
-  bool fill3 = false, rng_dirty = false;
+  bool fill3 = false, rng_dirty = false, rng_loaded = false;
   if (active) {
     float fx[4], fy[4], tq[4];
     load_scalars(S, e, E);
@@ -863,6 +863,14 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
 #pragma unroll
     for (int b = 0; b < 5; ++b) { pvx[b] = E.px[b]; pvy[b] = E.py[b]; }
     E.steps += 1;
+    // PCG64 state now if this step may respawn (ball within 30 px of a goal mouth — it moves
+    // ≤ 4 px per step — or the episode ends here): loaded at the end it is a dependent HBM
+    // read in the slowest waves, issued when the memory system is busiest
+    if (((E.px[4] < 40.0f || E.px[4] > 760.0f) && E.py[4] > 195.0f && E.py[4] < 405.0f) ||
+        (P.autoreset && P.max_steps > 0 && E.steps >= P.max_steps)) {
+      load_rng(S, e, E);
+      rng_loaded = true;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float F[3];
@@ -897,7 +905,7 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
     const bool done = P.max_steps > 0 && E.steps >= P.max_steps;
     float r = blue_reward(P, pvx, pvy, E.px, E.py, goal, false, 0, 0);
     if (goal) {
-      load_rng(S, e, E);
+      if (!rng_loaded) load_rng(S, e, E);
       rng_dirty = true;
       soft_reset_regs(E);
     }
@@ -913,7 +921,7 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
     fill3 = (E.meta & META_HE) != 0;
     if (done && P.autoreset) {
       // marl_vecenv.py:48-51: env.reset(options={"use_full_random_positions": True})
-      if (!rng_dirty) load_rng(S, e, E);
+      if (!rng_dirty && !rng_loaded) load_rng(S, e, E);
       rng_dirty = true;
       reset_env_regs(E, MS_SPAWN_FULL_RANDOM);
       fill3 = true;
