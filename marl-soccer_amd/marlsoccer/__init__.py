@@ -11,3 +11,4 @@ from .config import load_config, to_ms_config  # noqa: F401
 from . import _native  # noqa: F401
 
 __all__ = ["SoccerBatch", "StepOutput", "spawn_mode", "load_config", "to_ms_config"]
+# marlsoccer.rollout (Agent, RunningMeanStd, DeviceRollout): the device-resident policy loop

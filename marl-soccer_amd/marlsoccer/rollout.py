@@ -1,0 +1,186 @@
+"""Device-resident policy rollout for the soccer env.
+
+The reference's caller (marl-soccer.ipynb, the `train` cell) runs its PPO rollout on the host:
+every step it copies the observations to numpy, normalises them there, runs the policy, copies
+the actions back and builds a numpy (N, 4, 3) action array with uniform(-1, 1) actions for the
+two untrained red agents (notebook L289-336). Here the same loop stays on the GPU: obs ->
+normaliser -> actor/critic MLP (hipBLASLt GEMMs through torch) -> action assembly -> ms_step,
+with the rollout storage laid out exactly as the notebook's (num_steps, num_envs, 2, ...).
+
+Formats are the reference's, so its artefacts load unchanged:
+  * `Agent` has the notebook's / eval.py's module tree (critic.*, actor_mean.*, actor_logstd),
+    so `Agent.load_state_dict(torch.load(path, weights_only=True))` reads a reference
+    `*.ppo_model` checkpoint (eval.py:17-47, 58-60);
+  * `RunningMeanStd.save_npz/load_npz` use the `mean`, `var` float64 (66,) arrays of
+    `latest_normalizer_stats.npz` (notebook L455-458, eval.py:62-66).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.distributions.normal import Normal
+
+OBS_DIM, ACT_DIM = 66, 3
+TRAINABLE = (0, 1)   # agent_0, agent_1 (blue) — notebook L243
+RANDOM = (2, 3)      # red agents act uniformly at random — notebook L315-316
+
+
+class RunningMeanStd:
+    """Welford/Chan running moments, float64 on the device (notebook L190-222)."""
+
+    def __init__(self, shape=(OBS_DIM,), device=None):
+        self.device = torch.device("cpu") if device is None else torch.device(device)
+        self.mean = torch.zeros(shape, dtype=torch.float64, device=self.device)
+        self.var = torch.ones(shape, dtype=torch.float64, device=self.device)
+        self.count = 0
+
+    def update(self, x: torch.Tensor) -> None:
+        """x: (B, *shape). np.mean / np.var(ddof=0) of the batch, then the notebook's merge."""
+        x = x.to(self.device, torch.float64).reshape(-1, *self.mean.shape)
+        batch_mean = x.mean(dim=0)
+        batch_var = x.var(dim=0, unbiased=False)
+        batch_count = x.shape[0]
+        delta = batch_mean - self.mean
+        tot_count = self.count + batch_count
+        self.mean = self.mean + delta * batch_count / tot_count
+        m_a = self.var * self.count
+        m_b = batch_var * batch_count
+        m2 = m_a + m_b + torch.square(delta) * self.count * batch_count / tot_count
+        self.var = m2 / tot_count
+        self.count = tot_count
+
+    @property
+    def std(self) -> torch.Tensor:
+        return torch.sqrt(self.var)
+
+    def normalize(self, x: torch.Tensor) -> torch.Tensor:
+        """clip((x - mean) / (std + 1e-8), -10, 10), in float64 then float32 (notebook L301:
+        the rollout normalises the numpy float64 way before torch.tensor(..., dtype=float))."""
+        y = (x.to(torch.float64) - self.mean) / (self.std + 1e-8)
+        return torch.clamp(y, -10.0, 10.0).to(torch.float32)
+
+    def save_npz(self, path: str) -> None:
+        np.savez(path, mean=self.mean.cpu().numpy(), var=self.var.cpu().numpy())
+
+    @classmethod
+    def load_npz(cls, path: str, device=None) -> "RunningMeanStd":
+        with np.load(path) as d:  # allow_pickle=False (numpy default)
+            r = cls(tuple(d["mean"].shape), device)
+            r.mean = torch.as_tensor(np.asarray(d["mean"], np.float64), device=r.device)
+            r.var = torch.as_tensor(np.asarray(d["var"], np.float64), device=r.device)
+        return r
+
+
+def layer_init(layer: nn.Linear, std=np.sqrt(2), bias_const=0.0) -> nn.Linear:
+    nn.init.orthogonal_(layer.weight, std)
+    nn.init.constant_(layer.bias, bias_const)
+    return layer
+
+
+class Agent(nn.Module):
+    """The reference's actor-critic (notebook `Agent`, eval.py:17-47): two tanh MLPs
+    66-512-256-128-64-{1, 3} and a state-independent log-std."""
+
+    def __init__(self, obs_dim: int = OBS_DIM, act_dim: int = ACT_DIM, rpo_alpha: float = 0.0):
+        super().__init__()
+        self.critic = nn.Sequential(
+            layer_init(nn.Linear(obs_dim, 512)), nn.Tanh(),
+            nn.Linear(512, 256), nn.Tanh(), nn.Linear(256, 128), nn.Tanh(),
+            layer_init(nn.Linear(128, 64)), nn.Tanh(), layer_init(nn.Linear(64, 1), std=1.0),
+        )
+        self.actor_mean = nn.Sequential(
+            layer_init(nn.Linear(obs_dim, 512)), nn.Tanh(),
+            nn.Linear(512, 256), nn.Tanh(), nn.Linear(256, 128), nn.Tanh(),
+            layer_init(nn.Linear(128, 64)), nn.Tanh(), layer_init(nn.Linear(64, act_dim), std=0.01),
+        )
+        self.actor_logstd = nn.Parameter(torch.zeros(1, act_dim))
+        self.rpo_alpha = rpo_alpha
+
+    def get_value(self, x: torch.Tensor) -> torch.Tensor:
+        return self.critic(x)
+
+    def get_action_and_value(self, x: torch.Tensor, action: torch.Tensor | None = None, generator=None):
+        """notebook `get_action_and_value` (RPO: uniform(-alpha, alpha) jitter of the mean when
+        re-evaluating a given action)."""
+        action_mean = self.actor_mean(x)
+        action_std = torch.exp(self.actor_logstd.expand_as(action_mean))
+        if action is None:
+            action = torch.normal(action_mean, action_std, generator=generator)
+        else:
+            z = (torch.rand(action_mean.shape, device=action_mean.device, generator=generator) * 2 - 1) * self.rpo_alpha
+            action_mean = action_mean + z
+        probs = Normal(action_mean, action_std)
+        return action, probs.log_prob(action).sum(1), probs.entropy().sum(1), self.critic(x)
+
+    def get_deterministic_action(self, x: torch.Tensor) -> torch.Tensor:
+        return self.actor_mean(x)
+
+
+class DeviceRollout:
+    """The notebook's rollout phase (L289-336) with every tensor on the env's device.
+
+    collect() runs num_steps env steps and returns the PPO storage
+    {obs, actions, logprobs, rewards, dones, values} shaped (num_steps, N, 2, ...) like the
+    notebook's, plus next_obs / next_done for bootstrapping, the number of finished env
+    episodes and the sum of their final (blue, red) scores.
+    deterministic=True uses the actor mean (eval.py:79-81) instead of sampling.
+    """
+
+    def __init__(self, batch, agent: Agent, normalizer: RunningMeanStd, num_steps: int, seed: int = 0,
+                 deterministic: bool = False, update_normalizer: bool = True):
+        self.batch, self.agent, self.normalizer = batch, agent, normalizer
+        self.T, self.N = int(num_steps), batch.num_envs
+        self.deterministic = deterministic
+        self.update_normalizer = update_normalizer
+        dev = batch.device
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(seed)
+        T, N = self.T, self.N
+        self.obs = torch.zeros((T, N, 2, OBS_DIM), dtype=torch.float32, device=dev)
+        self.actions = torch.zeros((T, N, 2, ACT_DIM), dtype=torch.float32, device=dev)
+        self.logprobs = torch.zeros((T, N, 2), dtype=torch.float32, device=dev)
+        self.rewards = torch.zeros((T, N, 2), dtype=torch.float32, device=dev)
+        self.dones = torch.zeros((T, N, 2), dtype=torch.float32, device=dev)
+        self.values = torch.zeros((T, N, 2), dtype=torch.float32, device=dev)
+        self.full_actions = torch.zeros((N, 4, ACT_DIM), dtype=torch.float32, device=dev)
+        self.next_obs = batch.obs[:, list(TRAINABLE)].clone()
+        self.next_done = torch.zeros((N, 2), dtype=torch.float32, device=dev)
+        self.episodes = torch.zeros((), dtype=torch.int64, device=dev)  # finished env episodes
+        self.score_sum = torch.zeros((2,), dtype=torch.int64, device=dev)
+
+    @torch.no_grad()
+    def step(self, t: int) -> None:
+        b = self.batch
+        self.obs[t] = self.next_obs
+        self.dones[t] = self.next_done
+        x = self.normalizer.normalize(self.next_obs.reshape(-1, OBS_DIM))
+        if self.deterministic:
+            action = self.agent.get_deterministic_action(x)
+            value = self.agent.get_value(x)
+            logprob = torch.zeros(x.shape[0], device=x.device)
+        else:
+            action, logprob, _, value = self.agent.get_action_and_value(x, generator=self.gen)
+        self.values[t] = value.reshape(self.N, 2)
+        self.actions[t] = action.reshape(self.N, 2, ACT_DIM)
+        self.logprobs[t] = logprob.reshape(self.N, 2)
+        fa = self.full_actions
+        fa[:, :2] = self.actions[t]
+        fa[:, 2:] = torch.rand((self.N, 2, ACT_DIM), generator=self.gen, device=fa.device) * 2.0 - 1.0
+        b.step_into(fa, b.obs, b.rew, b.term, b.trunc, b.goal, b.score)
+        self.rewards[t] = b.rew[:, :2]
+        self.next_obs.copy_(b.obs[:, :2])
+        done = (b.term[:, :2] | b.trunc[:, :2]).to(torch.float32)
+        self.next_done.copy_(done)
+        finished = b.trunc[:, 0].to(torch.bool)  # episodes end together for all four agents
+        self.episodes += finished.sum()
+        self.score_sum += (b.score * finished[:, None]).sum(dim=0)
+
+    def collect(self) -> dict:
+        for t in range(self.T):
+            self.step(t)
+        if self.update_normalizer:  # notebook L347: after the rollout, from the raw observations
+            self.normalizer.update(self.obs.reshape(-1, OBS_DIM))
+        return {"obs": self.obs, "actions": self.actions, "logprobs": self.logprobs, "rewards": self.rewards,
+                "dones": self.dones, "values": self.values, "next_obs": self.next_obs, "next_done": self.next_done,
+                "episodes": self.episodes, "score_sum": self.score_sum}

@@ -1,0 +1,128 @@
+"""Policy-side formats and the device rollout.
+
+CPU: marlsoccer.rollout.Agent and RunningMeanStd against golden vectors produced by the
+reference notebook's own classes (tests/golden/make_policy_fixture.py), and compatibility
+with the reference's run5 checkpoint / normaliser formats.
+GPU: DeviceRollout drives SoccerBatch with the policy on the device.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+from make_policy_fixture import rms_batches  # noqa: E402  (the batch generator, no reference code)
+
+from marlsoccer.rollout import Agent, DeviceRollout, RunningMeanStd  # noqa: E402
+
+FX = np.load(os.path.join(HERE, "golden", "policy.npz"))
+
+
+def test_agent_matches_reference_network():
+    torch.manual_seed(0)
+    agent = Agent()
+    x, a = torch.from_numpy(FX["x"]), torch.from_numpy(FX["a"])
+    with torch.no_grad():
+        np.testing.assert_array_equal(agent.actor_mean(x).numpy(), FX["mean"])
+        np.testing.assert_array_equal(agent.get_value(x).numpy(), FX["value"])
+        _, logprob, entropy, _ = agent.get_action_and_value(x, a)
+    np.testing.assert_array_equal(logprob.numpy(), FX["logprob"])
+    np.testing.assert_array_equal(entropy.numpy(), FX["entropy"])
+
+
+def test_agent_state_dict_matches_reference_checkpoint():
+    sd = Agent().state_dict()
+    keys = [str(k) for k in FX["ckpt_keys"]]
+    shapes = json.loads(str(FX["ckpt_shapes"]))
+    assert sorted(sd.keys()) == keys
+    assert [list(sd[k].shape) for k in keys] == shapes
+
+
+def test_running_mean_std_matches_notebook():
+    rms = RunningMeanStd((66,))
+    for b, m, v in zip(rms_batches(), FX["rms_means"], FX["rms_vars"]):
+        rms.update(torch.from_numpy(b))
+        np.testing.assert_allclose(rms.mean.numpy(), m, rtol=0, atol=1e-12)
+        np.testing.assert_allclose(rms.var.numpy(), v, rtol=1e-12, atol=1e-12)
+    assert rms.count == int(FX["rms_batch_sizes"].sum())
+
+
+def test_normaliser_npz_roundtrip_and_formula(tmp_path):
+    rms = RunningMeanStd((66,))
+    rms.mean = torch.from_numpy(FX["run5_mean"].copy())
+    rms.var = torch.from_numpy(FX["run5_var"].copy())
+    path = str(tmp_path / "latest_normalizer_stats.npz")
+    rms.save_npz(path)
+    with np.load(path) as d:
+        assert sorted(d.files) == ["mean", "var"] and d["mean"].dtype == np.float64 and d["mean"].shape == (66,)
+    back = RunningMeanStd.load_npz(path)
+    np.testing.assert_array_equal(back.var.numpy(), FX["run5_var"])
+    obs = np.random.default_rng(3).normal(size=(16, 66)).astype(np.float32) * 2
+    # eval.py:63-64, notebook L301: numpy float64 normalisation, clipped, then float32
+    want = np.clip((obs - FX["run5_mean"]) / (np.sqrt(FX["run5_var"]) + 1e-8), -10, 10).astype(np.float32)
+    np.testing.assert_array_equal(back.normalize(torch.from_numpy(obs)).numpy(), want)
+
+
+@pytest.mark.gpu
+def test_device_rollout_drives_env_on_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer import SoccerBatch
+    N, T = 512, 40
+    b = SoccerBatch(N)
+    b.reset(seed=19)
+    torch.manual_seed(0)
+    agent = Agent().cuda()
+    rms = RunningMeanStd((66,), device="cuda")
+    ro = DeviceRollout(b, agent, rms, T, seed=5)
+    first_obs = b.obs[:, :2].clone()
+    out = ro.collect()
+    torch.cuda.synchronize()
+    assert out["obs"].shape == (T, N, 2, 66) and out["actions"].shape == (T, N, 2, 3)
+    assert torch.equal(out["obs"][0], first_obs)
+    assert torch.equal(out["next_obs"], b.obs[:, :2])
+    assert torch.equal(out["rewards"][-1], b.rew[:, :2])
+    red = ro.full_actions[:, 2:]
+    assert float(red.min()) >= -1.0 and float(red.max()) <= 1.0 and float(red.std()) > 0.3
+    assert torch.isfinite(out["values"]).all() and torch.isfinite(out["logprobs"]).all()
+    assert rms.count == T * N * 2
+    # the policy saw exactly the normalised stored observations
+    with torch.no_grad():
+        x = RunningMeanStd((66,), device="cuda").normalize(out["obs"][3].reshape(-1, 66))
+        assert torch.allclose(agent.get_value(x).reshape(N, 2), out["values"][3], atol=1e-5, rtol=1e-5)
+    b.close()
+
+
+@pytest.mark.gpu
+def test_device_rollout_deterministic_matches_host_loop():
+    """Deterministic rollout == the eval.py-style host loop (policy mean for blue, the same
+    red actions) step for step."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer import SoccerBatch
+    N, T = 64, 12
+    torch.manual_seed(0)
+    agent = Agent().cuda()
+    rms = RunningMeanStd((66,), device="cuda")
+    b1, b2 = SoccerBatch(N), SoccerBatch(N)
+    b1.reset(seed=7)
+    b2.reset(seed=7)
+    ro = DeviceRollout(b1, agent, rms, T, seed=9, deterministic=True, update_normalizer=False)
+    out = ro.collect()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    for t in range(T):
+        with torch.no_grad():
+            mean = agent.actor_mean(rms.normalize(b2.obs[:, :2].reshape(-1, 66))).reshape(N, 2, 3)
+        acts = torch.empty((N, 4, 3), device="cuda")
+        acts[:, :2] = mean
+        acts[:, 2:] = torch.rand((N, 2, 3), generator=g, device="cuda") * 2.0 - 1.0
+        assert torch.equal(mean, out["actions"][t])
+        b2.step(acts)
+    assert torch.equal(b1.obs, b2.obs) and torch.equal(b1.rew, b2.rew)
+    b1.close()
+    b2.close()
