@@ -128,21 +128,27 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # The K launches go back to back on the env's stream, bracketed by ONE pair of HIP events:
+    # an event record between launches costs ~8 us of wall per step and perturbs the next
+    # kernel, so per-launch events would measure a slower loop than the one being timed.
+    # kernel_ms = event span / K is therefore the per-launch time including the (small)
+    # dispatch gap between consecutive kernels — an upper bound on the kernel duration;
+    # profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace) gives the exact one.
+    stream = batch.stream
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
-        ev[i][0].record(stream)
         launch(args.warmup + i)
-        ev[i][1].record(stream)
         if gathered is not None:
             dist.all_gather_into_tensor(gathered, obs)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if shared else dev)
@@ -187,6 +193,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "ms_step_kernel", "kernel_ms": kern_ms,
+                         "kernel_ms_method": "HIP events around the K back-to-back launches / K",
                          "alg_bytes_per_env_step": bytes_per_step,
                          "mean_cached_arbiters": mean_arb,  # sampled after the timed window
                          "pmc": pmc_info},
