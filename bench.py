@@ -61,9 +61,20 @@ def cpu_baseline(args):
     cores = max(1, min(cores, 16))
     n, k = args.cpu_envs, args.cpu_steps
     secs = orc.cpu_baseline(n, k, cores, "f64")
+    # also the serial one-env-at-a-time loop on one core
+    n1, k1 = 4096, 500
+    secs1 = orc.cpu_baseline(n1, k1, 1, "f64")
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except Exception:
+        pass
     return {"value": n * k / secs, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "sample": f"oracle f64 (C restatement of Game.step + Chipmunk) {n} envs x {k} steps, "
-                      f"random actions, {cores} threads, {secs:.2f} s wall"}
+                      f"random actions, {cores} threads, {secs:.2f} s wall",
+            "single_core": {"value": n1 * k1 / secs1, "sample": f"{n1} envs x {k1} steps, 1 thread, {secs1:.2f} s"},
+            "host": {"cpu_count": os.cpu_count(), "model": model}}
 
 
 def load_pmc_traffic():

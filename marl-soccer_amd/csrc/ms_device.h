@@ -37,18 +37,23 @@ struct Params {
 // ------------------------------------------------------------------------------------------
 // cpVect helpers (Chipmunk chipmunk_types.h / cpVect.h semantics)
 // ------------------------------------------------------------------------------------------
-struct V2 {
-  float x, y;
-};
+// 2-vectors as a clang vector type: every x/y pair operation below is one packed fp32
+// instruction (v_pk_add_f32 / v_pk_mul_f32, per-half negation as a source modifier). Each
+// component is the same IEEE operation on the same operands as the scalar formula (no
+// contraction: -ffp-contract=off), so results are bit-identical to the scalar restatement.
+typedef float V2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ V2 v2(float x, float y) { return V2{x, y}; }
-__device__ __forceinline__ V2 vadd(V2 a, V2 b) { return v2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ V2 vsub(V2 a, V2 b) { return v2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ V2 vneg(V2 a) { return v2(-a.x, -a.y); }
-__device__ __forceinline__ V2 vmult(V2 a, float s) { return v2(a.x * s, a.y * s); }
-__device__ __forceinline__ float vdot(V2 a, V2 b) { return a.x * b.x + a.y * b.y; }
-__device__ __forceinline__ float vcross(V2 a, V2 b) { return a.x * b.y - a.y * b.x; }
+__device__ __forceinline__ V2 vadd(V2 a, V2 b) { return a + b; }
+__device__ __forceinline__ V2 vsub(V2 a, V2 b) { return a - b; }
+__device__ __forceinline__ V2 vneg(V2 a) { return -a; }
+__device__ __forceinline__ V2 vmult(V2 a, float s) { return a * s; }
+// a.x * b.x + a.y * b.y
+__device__ __forceinline__ float vdot(V2 a, V2 b) { const V2 p = a * b; return p.x + p.y; }
+// a.x * b.y - a.y * b.x
+__device__ __forceinline__ float vcross(V2 a, V2 b) { const V2 p = a * b.yx; return p.x - p.y; }
 __device__ __forceinline__ V2 vperp(V2 a) { return v2(-a.y, a.x); }
-__device__ __forceinline__ V2 vrotate(V2 a, V2 b) { return v2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+// (a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); x * -1 is an exact sign flip
+__device__ __forceinline__ V2 vrotate(V2 a, V2 b) { return a.x * b + (a.y * b.yx) * V2{-1.0f, 1.0f}; }
 __device__ __forceinline__ float vlengthsq(V2 a) { return vdot(a, a); }
 __device__ __forceinline__ float fmaxr(float a, float b) { return (a > b) ? a : b; }  // cpfmax
 __device__ __forceinline__ float fminr(float a, float b) { return (a < b) ? a : b; }  // cpfmin

@@ -34,7 +34,7 @@ using namespace ms;
 #define MS_BLOCK 64
 #endif
 #ifndef MS_ABLATE
-#define MS_ABLATE 0  // diagnostic builds only: 1 no solver, 2 no narrowphase, 3 no obs stores
+#define MS_ABLATE 0  // diagnostic builds only: 1 no solver, 2 no narrowphase, 3 no obs stores, 4 no arbiter cache, 5 no history loads
 #endif
 #define MAXA MS_MAX_ARBITERS
 
@@ -140,15 +140,19 @@ __device__ __forceinline__ void store_rng(const DevState& S, int64_t e, Env& E) 
 }
 
 // ---- LDS scratchpad ------------------------------------------------------------------------
-// Layouts are [field][index][lane]: the 64 lanes of a wave hit 64 distinct dwords whatever
-// body/box each lane selects, so dynamic per-lane indexing is bank-conflict free.
-enum { SV_VX = 0, SV_VY, SV_W, SV_VBX, SV_VBY, SV_WB, SV_PX, SV_PY, SV_N };
+// Layouts are [field][index][lane]: the 64 lanes of a wave hit 64 distinct dwords (or 8-byte
+// pairs) whatever body/box each lane selects, so dynamic per-lane indexing is conflict free.
+// x/y pairs are stored together so that they load into register pairs for packed math.
 enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
 
 struct Lds {
   Seg seg[8];  // static segments (walls, goal lines), read with per-lane indices
   struct {
-    float v[SV_N][6][MS_BLOCK];    // body p, v, w, v_bias, w_bias (body 5 = static, all 0)
+    V2 p[6][MS_BLOCK];             // body position (body 5 = static, all 0)
+    V2 v[6][MS_BLOCK];             // velocity
+    V2 vb[6][MS_BLOCK];            // bias velocity
+    float w[6][MS_BLOCK];          // angular velocity
+    float wb[6][MS_BLOCK];         // bias angular velocity
     float box[BX_N][4][MS_BLOCK];  // agent box transform (p, cos, sin)
   } ph;
 };
@@ -203,6 +207,8 @@ __device__ __forceinline__ void snap_store(const DevState& S, int64_t e, int slo
     p[(int64_t)(18 + i) * S.n] = s.ang[i]; p[(int64_t)(22 + i) * S.n] = s.w[i];
   }
 }
+// 22 floats at a 8-B aligned address: five 16-B stores and one 8-B store, the 8-B one first
+// when the frame starts half-way into a 16-B word
 // 22 floats at a 8-B aligned address: five 16-B stores and one 8-B store, the 8-B one first
 // when the frame starts half-way into a 16-B word
 template <bool ALIGNED16>
@@ -366,8 +372,8 @@ __device__ __forceinline__ void stage_segments(const Params& P, Lds& L, int lane
 // ---- physics: cpSpaceStep restated ---------------------------------------------------------
 // One contact of the per-step arbiter list (cpArbiter + cpContact fields the solver uses).
 struct CSlot {
-  float r1x, r1y, r2x, r2y, nx, ny, u;
-  float nMass, tMass, bias, bounce, jn, jt, jb;
+  V2 r1, r2, n;
+  float u, nMass, tMass, bias, bounce, jn, jt, jb;
   uint32_t m;  // ba 0-2 | bb 3-5 | warm 6 | cidx 7 | count 8-9 | hash 10-17 | cache pos 18-23 | pair 24-29
 };
 #define CS_BA(m) ((int)((m) & 7u))
@@ -406,8 +412,7 @@ struct Contacts {
 // lets the optimizer merge the KREG stores into one store through a phi of slot pointers,
 // which pins the slots in scratch memory.
 __device__ __forceinline__ void slot_select(CSlot& d, const CSlot& s, bool c) {
-  d.r1x = c ? s.r1x : d.r1x; d.r1y = c ? s.r1y : d.r1y; d.r2x = c ? s.r2x : d.r2x; d.r2y = c ? s.r2y : d.r2y;
-  d.nx = c ? s.nx : d.nx; d.ny = c ? s.ny : d.ny; d.u = c ? s.u : d.u;
+  d.r1 = c ? s.r1 : d.r1; d.r2 = c ? s.r2 : d.r2; d.n = c ? s.n : d.n; d.u = c ? s.u : d.u;
   d.nMass = c ? s.nMass : d.nMass; d.tMass = c ? s.tMass : d.tMass; d.bias = c ? s.bias : d.bias;
   d.bounce = c ? s.bounce : d.bounce; d.jn = c ? s.jn : d.jn; d.jt = c ? s.jt : d.jt; d.jb = c ? s.jb : d.jb;
   d.m = c ? s.m : d.m;
@@ -437,12 +442,11 @@ __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds
   const int p = CS_PAIR(c.m);
   const float e_s = ((p - 10) & 7) < 6 ? P.e_aw : P.e_ag;
   const float e = p < 6 ? P.e_aa : (p < 10 ? P.e_ab : (p < 42 ? e_s : P.e_bw));
-  const V2 n = v2(c.nx, c.ny);
-  const V2 body_delta = v2(L.ph.v[SV_PX][bb][lane] - L.ph.v[SV_PX][ba][lane], L.ph.v[SV_PY][bb][lane] - L.ph.v[SV_PY][ba][lane]);
-  const V2 va = v2(L.ph.v[SV_VX][ba][lane], L.ph.v[SV_VY][ba][lane]);
-  const V2 vb = v2(L.ph.v[SV_VX][bb][lane], L.ph.v[SV_VY][bb][lane]);
-  const float wa = L.ph.v[SV_W][ba][lane], wbv = L.ph.v[SV_W][bb][lane];
-  const V2 r1 = v2(c.r1x, c.r1y), r2 = v2(c.r2x, c.r2y);
+  const V2 n = c.n;
+  const V2 body_delta = L.ph.p[bb][lane] - L.ph.p[ba][lane];
+  const V2 va = L.ph.v[ba][lane], vb = L.ph.v[bb][lane];
+  const float wa = L.ph.w[ba][lane], wbv = L.ph.w[bb][lane];
+  const V2 r1 = c.r1, r2 = c.r2;
   const float rcn1 = vcross(r1, n), rcn2 = vcross(r2, n);
   c.nMass = 1.0f / ((ma + ia * rcn1 * rcn1) + (mb + ib * rcn2 * rcn2));
   const V2 t = vperp(n);
@@ -461,30 +465,28 @@ __device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L
   if (!CS_WARM(c.m)) return;
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
   const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_minv(P, bb), ib = body_iinv(P, bb);
-  const V2 j = vrotate(v2(c.nx, c.ny), v2(c.jn, c.jt));
+  const V2 j = vrotate(c.n, v2(c.jn, c.jt));
   const V2 nj = vneg(j);
-  L.ph.v[SV_VX][ba][lane] = L.ph.v[SV_VX][ba][lane] + nj.x * ma;
-  L.ph.v[SV_VY][ba][lane] = L.ph.v[SV_VY][ba][lane] + nj.y * ma;
-  L.ph.v[SV_W][ba][lane] += ia * vcross(v2(c.r1x, c.r1y), nj);
-  L.ph.v[SV_VX][bb][lane] = L.ph.v[SV_VX][bb][lane] + j.x * mb;
-  L.ph.v[SV_VY][bb][lane] = L.ph.v[SV_VY][bb][lane] + j.y * mb;
-  L.ph.v[SV_W][bb][lane] += ib * vcross(v2(c.r2x, c.r2y), j);
+  L.ph.v[ba][lane] = L.ph.v[ba][lane] + vmult(nj, ma);
+  L.ph.w[ba][lane] += ia * vcross(c.r1, nj);
+  L.ph.v[bb][lane] = L.ph.v[bb][lane] + vmult(j, mb);
+  L.ph.w[bb][lane] += ib * vcross(c.r2, j);
 }
 
 // cpArbiterApplyImpulse for one contact
 __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int lane) {
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
   const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_minv(P, bb), ib = body_iinv(P, bb);
-  const V2 n = v2(c.nx, c.ny);
-  const V2 r1 = v2(c.r1x, c.r1y), r2 = v2(c.r2x, c.r2y);
-  const float vbxa = L.ph.v[SV_VBX][ba][lane], vbya = L.ph.v[SV_VBY][ba][lane], wba = L.ph.v[SV_WB][ba][lane];
-  const float vbxb = L.ph.v[SV_VBX][bb][lane], vbyb = L.ph.v[SV_VBY][bb][lane], wbb = L.ph.v[SV_WB][bb][lane];
-  const float vxa = L.ph.v[SV_VX][ba][lane], vya = L.ph.v[SV_VY][ba][lane], wa = L.ph.v[SV_W][ba][lane];
-  const float vxb = L.ph.v[SV_VX][bb][lane], vyb = L.ph.v[SV_VY][bb][lane], wb_ = L.ph.v[SV_W][bb][lane];
-  const V2 vb1 = vadd(v2(vbxa, vbya), vmult(vperp(r1), wba));
-  const V2 vb2 = vadd(v2(vbxb, vbyb), vmult(vperp(r2), wbb));
-  const V2 vs1 = vadd(v2(vxa, vya), vmult(vperp(r1), wa));
-  const V2 vs2 = vadd(v2(vxb, vyb), vmult(vperp(r2), wb_));
+  const V2 n = c.n;
+  const V2 r1 = c.r1, r2 = c.r2;
+  const V2 vba = L.ph.vb[ba][lane], vbb = L.ph.vb[bb][lane];
+  const float wba = L.ph.wb[ba][lane], wbb = L.ph.wb[bb][lane];
+  const V2 va = L.ph.v[ba][lane], vb = L.ph.v[bb][lane];
+  const float wa = L.ph.w[ba][lane], wb_ = L.ph.w[bb][lane];
+  const V2 vb1 = vadd(vba, vmult(vperp(r1), wba));
+  const V2 vb2 = vadd(vbb, vmult(vperp(r2), wbb));
+  const V2 vs1 = vadd(va, vmult(vperp(r1), wa));
+  const V2 vs2 = vadd(vb, vmult(vperp(r2), wb_));
   const V2 vr = vsub(vs2, vs1);
   const float vbn = vdot(vsub(vb2, vb1), n);
   const float vrn = vdot(vr, n);
@@ -509,18 +511,14 @@ __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int
   const V2 nj = vneg(j);
   // body a first, then body b (apply_bias_impulses then apply_impulses, cpArbiter.c);
   // a and b are distinct bodies, so the four updates commute per body.
-  L.ph.v[SV_VBX][ba][lane] = vbxa + njb.x * ma;
-  L.ph.v[SV_VBY][ba][lane] = vbya + njb.y * ma;
-  L.ph.v[SV_WB][ba][lane] = wba + ia * vcross(r1, njb);
-  L.ph.v[SV_VBX][bb][lane] = vbxb + jbv.x * mb;
-  L.ph.v[SV_VBY][bb][lane] = vbyb + jbv.y * mb;
-  L.ph.v[SV_WB][bb][lane] = wbb + ib * vcross(r2, jbv);
-  L.ph.v[SV_VX][ba][lane] = vxa + nj.x * ma;
-  L.ph.v[SV_VY][ba][lane] = vya + nj.y * ma;
-  L.ph.v[SV_W][ba][lane] = wa + ia * vcross(r1, nj);
-  L.ph.v[SV_VX][bb][lane] = vxb + j.x * mb;
-  L.ph.v[SV_VY][bb][lane] = vyb + j.y * mb;
-  L.ph.v[SV_W][bb][lane] = wb_ + ib * vcross(r2, j);
+  L.ph.vb[ba][lane] = vadd(vba, vmult(njb, ma));
+  L.ph.wb[ba][lane] = wba + ia * vcross(r1, njb);
+  L.ph.vb[bb][lane] = vadd(vbb, vmult(jbv, mb));
+  L.ph.wb[bb][lane] = wbb + ib * vcross(r2, jbv);
+  L.ph.v[ba][lane] = vadd(va, vmult(nj, ma));
+  L.ph.w[ba][lane] = wa + ia * vcross(r1, nj);
+  L.ph.v[bb][lane] = vadd(vb, vmult(j, mb));
+  L.ph.w[bb][lane] = wb_ + ib * vcross(r2, j);
 }
 
 __device__ __forceinline__ void lds_box(const Lds& L, int i, int lane, Box& b) {
@@ -573,17 +571,16 @@ __device__ __forceinline__ void add_arbiter(const DevState& S, int64_t e, const 
   int pos = W.out;
   if (W.out < MAXA) ++W.out; else { (*overflow_acc)++; pos = 63; }
   C.na++;
-  const float ax = L.ph.v[SV_PX][ba][lane], ay = L.ph.v[SV_PY][ba][lane];
-  const float bx = L.ph.v[SV_PX][bb][lane], by = L.ph.v[SV_PY][bb][lane];
+  const V2 pa = L.ph.p[ba][lane], pb = L.ph.p[bb][lane];
   const uint32_t warm = (found && ((oh >> 8) & 3u) == 0u) ? 1u : 0u;
   for (int k = 0; k < col.count; ++k) {
     CSlot s;
     const V2 p1 = k == 0 ? col.p1[0] : col.p1[1];
     const V2 p2 = k == 0 ? col.p2[0] : col.p2[1];
     const int h = k == 0 ? col.hash[0] : col.hash[1];
-    s.r1x = p1.x - ax; s.r1y = p1.y - ay;
-    s.r2x = p2.x - bx; s.r2y = p2.y - by;
-    s.nx = col.n.x; s.ny = col.n.y; s.u = u;
+    s.r1 = vsub(p1, pa);
+    s.r2 = vsub(p2, pb);
+    s.n = col.n; s.u = u;
     s.nMass = 0.0f; s.tMass = 0.0f; s.bias = 0.0f; s.bounce = 0.0f; s.jb = 0.0f;
     s.jn = 0.0f; s.jt = 0.0f;
     if (found) {
@@ -650,12 +647,12 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
   }
 #pragma unroll
   for (int b = 0; b < 5; ++b) {
-    L.ph.v[SV_PX][b][lane] = E.px[b]; L.ph.v[SV_PY][b][lane] = E.py[b];
-    L.ph.v[SV_VX][b][lane] = E.vx[b]; L.ph.v[SV_VY][b][lane] = E.vy[b]; L.ph.v[SV_W][b][lane] = E.w[b];
-    L.ph.v[SV_VBX][b][lane] = 0.0f; L.ph.v[SV_VBY][b][lane] = 0.0f; L.ph.v[SV_WB][b][lane] = 0.0f;
+    L.ph.p[b][lane] = v2(E.px[b], E.py[b]);
+    L.ph.v[b][lane] = v2(E.vx[b], E.vy[b]); L.ph.w[b][lane] = E.w[b];
+    L.ph.vb[b][lane] = v2(0.0f, 0.0f); L.ph.wb[b][lane] = 0.0f;
   }
-#pragma unroll
-  for (int f = 0; f < SV_N; ++f) L.ph.v[f][5][lane] = 0.0f;
+  L.ph.p[5][lane] = v2(0.0f, 0.0f); L.ph.v[5][lane] = v2(0.0f, 0.0f); L.ph.vb[5][lane] = v2(0.0f, 0.0f);
+  L.ph.w[5][lane] = 0.0f; L.ph.wb[5][lane] = 0.0f;
   const V2 ballc = v2(E.px[4], E.py[4]);
   const float BR = 10.0f;
   const float ballbb[4] = {ballc.x - BR, ballc.y - BR, ballc.x + BR, ballc.y + BR};
@@ -690,6 +687,9 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
   CacheWalk W;
   W.par = (E.meta & META_PAR) ? 1 : 0;
   W.nc_old = META_NC(E.meta);
+#if MS_ABLATE == 4  // old arbiter cache ignored (timing ablation)
+  W.nc_old = 0;
+#endif
   W.cur = 0;
   W.out = 0;
   W.curh = W.nc_old > 0 ? S.CH[(int64_t)(W.par * MAXA + 0) * S.n + e] : 0xffffffffu;
@@ -717,6 +717,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     col_circle_box(ballc, BR, B, col);
     if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, 6 + i, 4, i, col, P.u_ab, overflow_acc);
   }
+  STAMP(11);
   while (mSA) {
     const int q = __builtin_ctz(mSA);
     mSA &= mSA - 1;
@@ -728,6 +729,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     col_seg_box(sg, B, col);
     if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, 10 + q, 5, i, col, s < 6 ? P.u_aw : P.u_ag, overflow_acc);
   }
+  STAMP(13);
   while (mBS) {
     const int s = __builtin_ctz(mBS);
     mBS &= mBS - 1;
@@ -748,6 +750,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
 
   // cpArbiterPreStep
   FOR_CONTACTS(C, ovf, prestep_one(P, c_, L, lane));
+  STAMP(14);
 
   // cpBodyUpdateVelocity + entities.py velocity_func (damping, max-velocity clamp)
 #pragma unroll
@@ -767,13 +770,14 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
       nvy = (nvy / len) * P.vmax;
     }
     E.vx[b] = nvx; E.vy[b] = nvy; E.w[b] = nw;
-    L.ph.v[SV_VX][b][lane] = nvx; L.ph.v[SV_VY][b][lane] = nvy; L.ph.v[SV_W][b][lane] = nw;
+    L.ph.v[b][lane] = v2(nvx, nvy); L.ph.w[b][lane] = nw;
   }
 
   STAMP(4);
   if (C.nc > 0) {
     // cpArbiterApplyCachedImpulse, then cpArbiterApplyImpulse x 10 (pymunk Space default)
     FOR_CONTACTS(C, ovf, warm_one(P, c_, L, lane));
+    STAMP(15);
 #pragma unroll 1
     for (int it = 0; it < 10 * (MS_ABLATE != 1); ++it) {
       asm volatile("; MS_SOLVER_ITER_BEGIN" ::: "memory");
@@ -783,8 +787,9 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     STAMP(5);
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
-      E.vx[b] = L.ph.v[SV_VX][b][lane]; E.vy[b] = L.ph.v[SV_VY][b][lane]; E.w[b] = L.ph.v[SV_W][b][lane];
-      E.vbx[b] = L.ph.v[SV_VBX][b][lane]; E.vby[b] = L.ph.v[SV_VBY][b][lane]; E.wb[b] = L.ph.v[SV_WB][b][lane];
+      const V2 v = L.ph.v[b][lane], vbv = L.ph.vb[b][lane];
+      E.vx[b] = v.x; E.vy[b] = v.y; E.w[b] = L.ph.w[b][lane];
+      E.vbx[b] = vbv.x; E.vby[b] = vbv.y; E.wb[b] = L.ph.wb[b][lane];
     }
     // touched arbiters' cache entries at the positions reserved in merge order
     static_for<0, KREG - 1>([&](auto kc) __attribute__((always_inline)) {
@@ -832,9 +837,11 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
   bool active = e < S.n;
 
   // SoccerEnv.step validation + clip + fp32 scaling (soccer_env.py:101-125)
+  // the actions, scalars and bodies are loaded together: one memory round trip before physics
   float a[12];
 #pragma unroll
   for (int k = 0; k < 12; ++k) a[k] = 0.0f;
+  Env E;
   if (active) {
     const float4* ap = (const float4*)(actions + e * 12);
 #pragma unroll
@@ -842,6 +849,8 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
       float4 v = ap[q];
       a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
     }
+    load_scalars(S, e, E);
+    load_bodies(S, e, E);
     bool finite = true;
 #pragma unroll
     for (int k = 0; k < 12; ++k) finite = finite && isfinite(a[k]);
@@ -852,14 +861,11 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
     }
   }
   stage_segments(P, L, lane);
-  Env E;
   Snap h2, h1;  // obs history snapshots t-2, t-1
   float pvx[5], pvy[5];
   bool fill3 = false, rng_dirty = false, rng_loaded = false;
   if (active) {
     float fx[4], fy[4], tq[4];
-    load_scalars(S, e, E);
-    load_bodies(S, e, E);
 #pragma unroll
     for (int b = 0; b < 5; ++b) { pvx[b] = E.px[b]; pvy[b] = E.py[b]; }
     E.steps += 1;
@@ -893,8 +899,14 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
     if (ovf) atomicAdd(&ctr->overflow, ovf);
     {  // history snapshots: issued here so their latency hides under the reward math
       const int head = (E.meta & META_RING) ? 1 : 0;
+#if MS_ABLATE == 5  // history not loaded (timing ablation)
+      (void)head;
+      snap_of(E, h2);
+      snap_of(E, h1);
+#else
       snap_load(S, e, head ^ 1, h2);
       snap_load(S, e, head, h1);
+#endif
     }
 
     // goal detection (game.py:401-412)
