@@ -29,8 +29,10 @@ METRIC = "env-steps/sec (4 agents × N envs) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 # Algorithmic HBM bytes per env-step of ms_step_kernel (DESIGN.md "Roofline"):
-ALG_READ = 48 + 176 + 12 + 208      # actions, bodies, scalars, 2 obs-history snapshots (2 x 26 f32)
-ALG_WRITE = 176 + 12 + 104 + 1056 + 16 + 4 + 4 + 1 + 8  # bodies, scalars, new snapshot, obs, rew, term, trunc, goal, score
+# actions, bodies, scalars (steps, score, meta, PCG64 buffered u32), the t-2 obs-history snapshot
+# (26 f32; the t-1 snapshot is the body state itself)
+ALG_READ = 48 + 176 + 16 + 104
+ALG_WRITE = 176 + 16 + 104 + 1056 + 16 + 4 + 4 + 1 + 8  # bodies, scalars, snapshot, obs, rew, term, trunc, goal, score
 ARB_BYTES = 20                       # one cached arbiter: header + 4 impulses (read + rewritten)
 
 

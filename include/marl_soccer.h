@@ -177,6 +177,12 @@ typedef struct ms_env ms_env;
 /* Fill `cfg` with the reference defaults (config.json + code defaults). */
 void ms_config_default(ms_config *cfg);
 
+/* 1 when `cfg` selects the step kernel specialised for the reference's default physics and
+ * rewards (config.json, compile-time constants; only max_steps and autoreset may differ),
+ * 0 when the generic kernel (parameters from kernel arguments) runs; negative on error.
+ * Both kernels compute the same results. Host-only, no device needed. */
+int ms_config_specialised(const ms_config *cfg);
+
 /* Allocate device state for `n_envs` environments on HIP device `device`; launches
  * go to `stream` (a hipStream_t; NULL = null stream). The envs start reset with
  * OS-entropy seeds and the default random spawn, as Game.__init__ -> reset() does

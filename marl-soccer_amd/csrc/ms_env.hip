@@ -6,13 +6,16 @@
 // One lane owns one env for the whole step: the physics of one env is a short sequential
 // Gauss-Seidel solve over at most a few contacts, so parallelism comes from the batch.
 //
-// HBM layout (struct-of-arrays, every plane is N contiguous elements so a wavefront's
-// 64 lanes touch 64 consecutive words):
-//   F  float [PL_F][N]   bodies (44 planes) + obs-history snapshot ring (2 x 26 planes)
-//   I  int32 [PL_I][N]   steps, score, meta bits, PCG64 buffered u32
-//   R  u64   [4][N]      PCG64 state/increment (touched only by resets and goal respawns)
-//   CH u32   [2][MAXA][N] arbiter-cache headers, ping-pong by a per-env parity bit
-//   CJ float [2][MAXA][4][N] arbiter-cache accumulated impulses (jn0, jt0, jn1, jt1)
+// HBM layout: struct of 16-byte groups. Every group array is N contiguous 16-B elements, so
+// one wave-instruction moves 1 KiB of contiguous memory and fetches four fields per lane:
+//   B4 float4 [11][N]     bodies, flat field i in group i/4 (agent b: 9b + px py vx vy angle w
+//                         vbx vby wb; ball: 36 + px py vx vy w vbx vby wb)
+//   H4 float4 [7][N]      obs-history snapshot of step t-2 (26 floats, 2 pad). The snapshot of
+//                         t-1 is the body state itself at the start of the step.
+//   I4 int4   [N]         steps, score (blue | red << 16), meta bits, PCG64 buffered u32
+//   R2 u64x2  [2][N]      PCG64 (state hi, lo), (inc hi, lo): touched by resets and goal respawns
+//   CH u32    [2][MAXA][N] arbiter-cache headers, ping-pong by a per-env parity bit
+//   CJ float4 [2][MAXA][N] arbiter-cache accumulated impulses (jn0, jt0, jn1, jt1)
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -38,30 +41,27 @@ using namespace ms;
 #endif
 #define MAXA MS_MAX_ARBITERS
 
-// ---- plane indices -----------------------------------------------------------------------
+// ---- group indices -----------------------------------------------------------------------
 enum {
-  // agent b (0..3): base b*9: PX PY VX VY ANG W VBX VBY WB ; ball: base 36: PX PY VX VY W VBX VBY WB
-  F_BALL = 36,
-  F_SNAP = 44,                   // [slot 2][MS_SNAP_SIZE]: px[5] py[5] vx[4] vy[4] angle[4] w[4]
-  PL_F = 44 + 2 * MS_SNAP_SIZE   // 96
+  F_BALL = 36,      // flat body field of the ball's px (agent b: 9b)
+  G_BODY = 11,      // float4 groups of body state (44 floats)
+  G_SNAP = 7        // float4 groups of one snapshot (MS_SNAP_SIZE = 26 floats + 2 pad)
 };
-enum { I_STEPS = 0, I_SCORE = 1, I_META = 2, I_U32 = 3, PL_I = 4 };
-// META bits: 0-1 spawn mode, 2 hist_empty, 3 ring head (slot holding t-1), 4 cache parity,
-//            8-13 n_cache, 16 PCG64 has_uint32
+// META bits: 0-1 spawn mode, 2 hist_empty, 4 cache parity, 8-13 n_cache, 16 PCG64 has_uint32
 #define META_MODE(m) ((m) & 3)
 #define META_HE 4u
-#define META_RING 8u
 #define META_PAR 16u
 #define META_NC(m) (((m) >> 8) & 63)
 #define META_H32 (1u << 16)
 
 struct DevState {
   unsigned long long* stamps;  // MS_STAMPS diagnostic builds only: [wave][16] s_memtime
-  float* F;
-  int32_t* I;
-  uint64_t* R;
+  float4* B4;
+  float4* H4;
+  int4* I4;
+  ulonglong2* R2;
   uint32_t* CH;
-  float* CJ;
+  float4* CJ;
   void* SP;  // contact slots KREG.. of each env (pile-ups only): [env][MAXC - KREG] CSlot
   int64_t n;
 };
@@ -72,13 +72,14 @@ struct Counters {
   long long first_bad;
 };
 
-__device__ __forceinline__ float& AGF(const DevState& S, int b, int f, int64_t e) { return S.F[(int64_t)(b * 9 + f) * S.n + e]; }
 
 #ifdef MS_STAMPS
 #define STAMP(k)                                                                         \
   do {                                                                                   \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
-    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[(int64_t)(blockIdx.x) * 16 + (k)] = t_; \
+    const unsigned long long act_ = __ballot(1);                                          \
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)act_) - 1 && S.stamps)              \
+      S.stamps[(int64_t)(blockIdx.x) * 16 + (k)] = t_;                                   \
   } while (0)
 #else
 #define STAMP(k) do { } while (0)
@@ -92,50 +93,53 @@ struct Env {
   Rng rng;
 };
 
-__device__ __forceinline__ void load_bodies(const DevState& S, int64_t e, Env& E) {
+__device__ __forceinline__ void unpack_bodies(const float f[44], Env& E) {
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    E.px[b] = AGF(S, b, 0, e); E.py[b] = AGF(S, b, 1, e);
-    E.vx[b] = AGF(S, b, 2, e); E.vy[b] = AGF(S, b, 3, e);
-    E.ang[b] = AGF(S, b, 4, e); E.w[b] = AGF(S, b, 5, e);
-    E.vbx[b] = AGF(S, b, 6, e); E.vby[b] = AGF(S, b, 7, e); E.wb[b] = AGF(S, b, 8, e);
+    E.px[b] = f[9 * b + 0]; E.py[b] = f[9 * b + 1]; E.vx[b] = f[9 * b + 2]; E.vy[b] = f[9 * b + 3];
+    E.ang[b] = f[9 * b + 4]; E.w[b] = f[9 * b + 5];
+    E.vbx[b] = f[9 * b + 6]; E.vby[b] = f[9 * b + 7]; E.wb[b] = f[9 * b + 8];
   }
-  const int64_t n = S.n;
-  E.px[4] = S.F[(F_BALL + 0) * n + e]; E.py[4] = S.F[(F_BALL + 1) * n + e];
-  E.vx[4] = S.F[(F_BALL + 2) * n + e]; E.vy[4] = S.F[(F_BALL + 3) * n + e];
-  E.w[4] = S.F[(F_BALL + 4) * n + e];
-  E.vbx[4] = S.F[(F_BALL + 5) * n + e]; E.vby[4] = S.F[(F_BALL + 6) * n + e];
-  E.wb[4] = S.F[(F_BALL + 7) * n + e];
+  E.px[4] = f[F_BALL + 0]; E.py[4] = f[F_BALL + 1]; E.vx[4] = f[F_BALL + 2]; E.vy[4] = f[F_BALL + 3];
+  E.w[4] = f[F_BALL + 4]; E.vbx[4] = f[F_BALL + 5]; E.vby[4] = f[F_BALL + 6]; E.wb[4] = f[F_BALL + 7];
+}
+
+__device__ __forceinline__ void load_bodies(const DevState& S, int64_t e, Env& E) {
+  float f[44];
+#pragma unroll
+  for (int g = 0; g < G_BODY; ++g) {
+    const float4 v = S.B4[(int64_t)g * S.n + e];
+    f[4 * g] = v.x; f[4 * g + 1] = v.y; f[4 * g + 2] = v.z; f[4 * g + 3] = v.w;
+  }
+  unpack_bodies(f, E);
 }
 
 __device__ __forceinline__ void store_bodies(const DevState& S, int64_t e, const Env& E) {
+  float f[44];
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    AGF(S, b, 0, e) = E.px[b]; AGF(S, b, 1, e) = E.py[b];
-    AGF(S, b, 2, e) = E.vx[b]; AGF(S, b, 3, e) = E.vy[b];
-    AGF(S, b, 4, e) = E.ang[b]; AGF(S, b, 5, e) = E.w[b];
-    AGF(S, b, 6, e) = E.vbx[b]; AGF(S, b, 7, e) = E.vby[b]; AGF(S, b, 8, e) = E.wb[b];
+    f[9 * b + 0] = E.px[b]; f[9 * b + 1] = E.py[b]; f[9 * b + 2] = E.vx[b]; f[9 * b + 3] = E.vy[b];
+    f[9 * b + 4] = E.ang[b]; f[9 * b + 5] = E.w[b];
+    f[9 * b + 6] = E.vbx[b]; f[9 * b + 7] = E.vby[b]; f[9 * b + 8] = E.wb[b];
   }
-  const int64_t n = S.n;
-  S.F[(F_BALL + 0) * n + e] = E.px[4]; S.F[(F_BALL + 1) * n + e] = E.py[4];
-  S.F[(F_BALL + 2) * n + e] = E.vx[4]; S.F[(F_BALL + 3) * n + e] = E.vy[4];
-  S.F[(F_BALL + 4) * n + e] = E.w[4];
-  S.F[(F_BALL + 5) * n + e] = E.vbx[4]; S.F[(F_BALL + 6) * n + e] = E.vby[4];
-  S.F[(F_BALL + 7) * n + e] = E.wb[4];
+  f[F_BALL + 0] = E.px[4]; f[F_BALL + 1] = E.py[4]; f[F_BALL + 2] = E.vx[4]; f[F_BALL + 3] = E.vy[4];
+  f[F_BALL + 4] = E.w[4]; f[F_BALL + 5] = E.vbx[4]; f[F_BALL + 6] = E.vby[4]; f[F_BALL + 7] = E.wb[4];
+#pragma unroll
+  for (int g = 0; g < G_BODY; ++g) S.B4[(int64_t)g * S.n + e] = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
 }
 
 __device__ __forceinline__ void load_rng(const DevState& S, int64_t e, Env& E) {
-  const int64_t n = S.n;
-  E.rng.shi = S.R[0 * n + e]; E.rng.slo = S.R[1 * n + e];
-  E.rng.ihi = S.R[2 * n + e]; E.rng.ilo = S.R[3 * n + e];
+  const ulonglong2 st = S.R2[e], inc = S.R2[S.n + e];
+  E.rng.shi = st.x; E.rng.slo = st.y;
+  E.rng.ihi = inc.x; E.rng.ilo = inc.y;
   E.rng.has32 = (E.meta & META_H32) ? 1u : 0u;
-  E.rng.u32 = (uint32_t)S.I[I_U32 * n + e];
 }
 __device__ __forceinline__ void store_rng(const DevState& S, int64_t e, Env& E) {
-  const int64_t n = S.n;
-  S.R[0 * n + e] = E.rng.shi; S.R[1 * n + e] = E.rng.slo;
-  S.R[2 * n + e] = E.rng.ihi; S.R[3 * n + e] = E.rng.ilo;
-  S.I[I_U32 * n + e] = (int32_t)E.rng.u32;
+  ulonglong2 st, inc;
+  st.x = E.rng.shi; st.y = E.rng.slo;
+  inc.x = E.rng.ihi; inc.y = E.rng.ilo;
+  S.R2[e] = st;
+  S.R2[S.n + e] = inc;
   E.meta = (E.meta & ~META_H32) | (E.rng.has32 ? META_H32 : 0u);
 }
 
@@ -144,6 +148,12 @@ __device__ __forceinline__ void store_rng(const DevState& S, int64_t e, Env& E) 
 // pairs) whatever body/box each lane selects, so dynamic per-lane indexing is conflict free.
 // x/y pairs are stored together so that they load into register pairs for packed math.
 enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
+#ifndef MS_EARLY_OBS
+#define MS_EARLY_OBS 0
+#endif
+#ifndef KC
+#define KC 4  // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (rare)
+#endif
 
 struct Lds {
   Seg seg[8];  // static segments (walls, goal lines), read with per-lane indices
@@ -155,6 +165,9 @@ struct Lds {
     float wb[6][MS_BLOCK];         // bias angular velocity
     float box[BX_N][4][MS_BLOCK];  // agent box transform (p, cos, sin)
   } ph;
+  // previous step's arbiter cache, entries 0..KC-1 (loaded with the state at kernel start)
+  uint32_t ch[KC][MS_BLOCK];
+  float4 cj[KC][MS_BLOCK];
 };
 
 // Compile-time loop: every reg[] access below uses a constant index from the first IR on,
@@ -187,88 +200,108 @@ __device__ __forceinline__ void snap_of(const Env& E, Snap& s) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) { s.vx[i] = E.vx[i]; s.vy[i] = E.vy[i]; s.ang[i] = E.ang[i]; s.w[i] = E.w[i]; }
 }
-__device__ __forceinline__ void snap_load(const DevState& S, int64_t e, int slot, Snap& s) {
-  const float* p = S.F + (int64_t)(F_SNAP + slot * MS_SNAP_SIZE) * S.n + e;
+// the t-2 snapshot (H4): px[5] py[5] vx[4] vy[4] angle[4] w[4] in 7 float4 groups
+__device__ __forceinline__ void snap_load(const DevState& S, int64_t e, Snap& s) {
+  float f[28];
 #pragma unroll
-  for (int b = 0; b < 5; ++b) { s.px[b] = p[(int64_t)b * S.n]; s.py[b] = p[(int64_t)(5 + b) * S.n]; }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    s.vx[i] = p[(int64_t)(10 + i) * S.n]; s.vy[i] = p[(int64_t)(14 + i) * S.n];
-    s.ang[i] = p[(int64_t)(18 + i) * S.n]; s.w[i] = p[(int64_t)(22 + i) * S.n];
+  for (int g = 0; g < G_SNAP; ++g) {
+    const float4 v = S.H4[(int64_t)g * S.n + e];
+    f[4 * g] = v.x; f[4 * g + 1] = v.y; f[4 * g + 2] = v.z; f[4 * g + 3] = v.w;
   }
+#pragma unroll
+  for (int b = 0; b < 5; ++b) { s.px[b] = f[b]; s.py[b] = f[5 + b]; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { s.vx[i] = f[10 + i]; s.vy[i] = f[14 + i]; s.ang[i] = f[18 + i]; s.w[i] = f[22 + i]; }
 }
-__device__ __forceinline__ void snap_store(const DevState& S, int64_t e, int slot, const Snap& s) {
-  float* p = S.F + (int64_t)(F_SNAP + slot * MS_SNAP_SIZE) * S.n + e;
+__device__ __forceinline__ void snap_store(const DevState& S, int64_t e, const Snap& s) {
+  float f[28];
 #pragma unroll
-  for (int b = 0; b < 5; ++b) { p[(int64_t)b * S.n] = s.px[b]; p[(int64_t)(5 + b) * S.n] = s.py[b]; }
+  for (int b = 0; b < 5; ++b) { f[b] = s.px[b]; f[5 + b] = s.py[b]; }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    p[(int64_t)(10 + i) * S.n] = s.vx[i]; p[(int64_t)(14 + i) * S.n] = s.vy[i];
-    p[(int64_t)(18 + i) * S.n] = s.ang[i]; p[(int64_t)(22 + i) * S.n] = s.w[i];
-  }
+  for (int i = 0; i < 4; ++i) { f[10 + i] = s.vx[i]; f[14 + i] = s.vy[i]; f[18 + i] = s.ang[i]; f[22 + i] = s.w[i]; }
+  f[26] = 0.0f; f[27] = 0.0f;
+#pragma unroll
+  for (int g = 0; g < G_SNAP; ++g) S.H4[(int64_t)g * S.n + e] = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
 }
-// 22 floats at a 8-B aligned address: five 16-B stores and one 8-B store, the 8-B one first
-// when the frame starts half-way into a 16-B word
-// 22 floats at a 8-B aligned address: five 16-B stores and one 8-B store, the 8-B one first
-// when the frame starts half-way into a 16-B word
-template <bool ALIGNED16>
-__device__ __forceinline__ void store_frame22(float* __restrict__ d, const float* f) {
-  if constexpr (ALIGNED16) {
+#ifndef MS_NT_OBS
+#define MS_NT_OBS 0  // 1: obs stores non-temporal (variant switch)
+#endif
+typedef float F4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void obs_put(float4* d, float4 v) {
+  if constexpr (MS_NT_OBS) __builtin_nontemporal_store(F4v{v.x, v.y, v.z, v.w}, (F4v*)d);
+  else *d = v;
+}
+__device__ __forceinline__ void obs_put(float2* d, float2 v) {
+  if constexpr (MS_NT_OBS) __builtin_nontemporal_store(V2{v.x, v.y}, (V2*)d);
+  else *d = v;
+}
+
+// The six agent-agent vectors of a snapshot, computed once per pair: agent j's vector to agent
+// i is the exact negation of i's to j (IEEE a-b = -(b-a), same magnitude).
+template <bool FAST>
+__device__ __forceinline__ void pair_vectors(const Snap& s, float aa[6][3]) {
+  constexpr int PI_[6] = {0, 0, 0, 1, 1, 2}, PJ_[6] = {1, 2, 3, 2, 3, 3};
 #pragma unroll
-    for (int q = 0; q < 5; ++q) *(float4*)(d + 4 * q) = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
-    *(float2*)(d + 20) = make_float2(f[20], f[21]);
+  for (int p = 0; p < 6; ++p) unit_mag<FAST>(s.px[PJ_[p]] - s.px[PI_[p]], s.py[PJ_[p]] - s.py[PI_[p]], aa[p]);
+}
+
+// Agent A's 22-float frame of a snapshot (Game._get_observations, game.py:258-322), stored as
+// stacked-frame slot K (0 = t-2, 1 = t-1, 2 = t; soccer_env.py:130-140) of its 66-float row.
+// A mirrored pair vector is written as 0 - u so that a zero component stays +0 as the direct
+// evaluation gives.
+template <bool FAST, int A, int K>
+__device__ __forceinline__ void agent_frame_store(const Params& P, const Snap& s, const float aa[6][3],
+                                                  float* __restrict__ row0) {
+  // obs slots 4 (teammate), 7, 10 (opponents in index order) -> (pair, mirrored)
+  constexpr int TEAM = A ^ 1, O1 = A < 2 ? 2 : 0, O2 = A < 2 ? 3 : 1;
+  constexpr int OTH[3] = {TEAM, O1, O2};
+  float f[22];
+  if constexpr (FAST) {
+    f[0] = div_nr(s.vx[A], P.obs_vmax, rcp_nr(P.obs_vmax));
+    f[1] = div_nr(s.vy[A], P.obs_vmax, rcp_nr(P.obs_vmax));
+    f[3] = div_nr(s.w[A], P.obs_wmax, rcp_nr(P.obs_wmax));
   } else {
-    *(float2*)d = make_float2(f[0], f[1]);
+    f[0] = s.vx[A] / P.obs_vmax;
+    f[1] = s.vy[A] / P.obs_vmax;
+    f[3] = s.w[A] / P.obs_wmax;
+  }
+  f[2] = angle_obs<FAST>(s.ang[A]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int B = OTH[k];
+    const int lo = A < B ? A : B, hi = A < B ? B : A;
+    const int p = lo == 0 ? hi - 1 : (lo == 1 ? hi + 1 : 5);
+    if (A < B) {
+      f[4 + 3 * k] = aa[p][0]; f[5 + 3 * k] = aa[p][1];
+    } else {
+      f[4 + 3 * k] = 0.0f - aa[p][0]; f[5 + 3 * k] = 0.0f - aa[p][1];
+    }
+    f[6 + 3 * k] = aa[p][2];
+  }
+  unit_mag<FAST>(s.px[4] - s.px[A], s.py[4] - s.py[A], f + 13);
+  const float own_x = A < 2 ? 10.0f : 790.0f, opp_x = A < 2 ? 790.0f : 10.0f;
+  unit_mag<FAST>(own_x - s.px[A], 300.0f - s.py[A], f + 16);
+  unit_mag<FAST>(opp_x - s.px[A], 300.0f - s.py[A], f + 19);
+  float* d = row0 + A * 66 + K * 22;
+  if constexpr (((A + K) & 1) == 0) {  // 16-B aligned: five 16-B stores and one 8-B store
+#pragma unroll
+    for (int q = 0; q < 5; ++q) obs_put((float4*)(d + 4 * q), make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]));
+    obs_put((float2*)(d + 20), make_float2(f[20], f[21]));
+  } else {  // starts half-way into a 16-B word: the 8-B store first
+    obs_put((float2*)d, make_float2(f[0], f[1]));
 #pragma unroll
     for (int q = 0; q < 5; ++q)
-      *(float4*)(d + 2 + 4 * q) = make_float4(f[2 + 4 * q], f[3 + 4 * q], f[4 + 4 * q], f[5 + 4 * q]);
+      obs_put((float4*)(d + 2 + 4 * q), make_float4(f[2 + 4 * q], f[3 + 4 * q], f[4 + 4 * q], f[5 + 4 * q]));
   }
 }
 
-// The four agents' frames of one snapshot (Game._get_observations, game.py:258-322), stored
-// as stacked-frame slot K (0 = t-2, 1 = t-1, 2 = t; soccer_env.py:130-140) of every agent's
-// 66-float row. The six agent-agent vectors are computed once per pair: agent j's vector to
-// agent i is the exact negation of i's to j (IEEE a-b = -(b-a), same magnitude), written as
-// 0 - u so that a zero component stays +0 as the direct evaluation gives.
+// The four agents' frames of one snapshot, stored as slot K of every agent's row.
 template <bool FAST, int K>
 __device__ __forceinline__ void emit_snapshot_impl(const Params& P, const Snap& s, float* __restrict__ row0) {
-  constexpr int PI_[6] = {0, 0, 0, 1, 1, 2}, PJ_[6] = {1, 2, 3, 2, 3, 3};
   float aa[6][3];
-#pragma unroll
-  for (int p = 0; p < 6; ++p) unit_mag<FAST>(s.px[PJ_[p]] - s.px[PI_[p]], s.py[PJ_[p]] - s.py[PI_[p]], aa[p]);
+  pair_vectors<FAST>(s, aa);
   static_for<0, 4>([&](auto ac) __attribute__((always_inline)) {
-    constexpr int A = decltype(ac)::value;
-    // obs slots 4 (teammate), 7, 10 (opponents in index order) -> (pair, mirrored)
-    constexpr int TEAM = A ^ 1, O1 = A < 2 ? 2 : 0, O2 = A < 2 ? 3 : 1;
-    constexpr int OTH[3] = {TEAM, O1, O2};
-    float f[22];
-    if constexpr (FAST) {
-      f[0] = div_nr(s.vx[A], P.obs_vmax, rcp_nr(P.obs_vmax));
-      f[1] = div_nr(s.vy[A], P.obs_vmax, rcp_nr(P.obs_vmax));
-      f[3] = div_nr(s.w[A], P.obs_wmax, rcp_nr(P.obs_wmax));
-    } else {
-      f[0] = s.vx[A] / P.obs_vmax;
-      f[1] = s.vy[A] / P.obs_vmax;
-      f[3] = s.w[A] / P.obs_wmax;
-    }
-    f[2] = angle_obs<FAST>(s.ang[A]);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int B = OTH[k];
-      const int lo = A < B ? A : B, hi = A < B ? B : A;
-      const int p = lo == 0 ? hi - 1 : (lo == 1 ? hi + 1 : 5);
-      if (A < B) {
-        f[4 + 3 * k] = aa[p][0]; f[5 + 3 * k] = aa[p][1];
-      } else {
-        f[4 + 3 * k] = 0.0f - aa[p][0]; f[5 + 3 * k] = 0.0f - aa[p][1];
-      }
-      f[6 + 3 * k] = aa[p][2];
-    }
-    unit_mag<FAST>(s.px[4] - s.px[A], s.py[4] - s.py[A], f + 13);
-    const float own_x = A < 2 ? 10.0f : 790.0f, opp_x = A < 2 ? 790.0f : 10.0f;
-    unit_mag<FAST>(own_x - s.px[A], 300.0f - s.py[A], f + 16);
-    unit_mag<FAST>(opp_x - s.px[A], 300.0f - s.py[A], f + 19);
-    store_frame22<((A + K) & 1) == 0>(row0 + A * 66 + K * 22, f);
+    agent_frame_store<FAST, decltype(ac)::value, K>(P, s, aa, row0);
   });
 }
 
@@ -300,30 +333,43 @@ __device__ __forceinline__ void emit_snapshot(const Params& P, const Snap& s, fl
   else emit_snapshot_impl<false, K>(P, s, row0);
 }
 
-// Obs output + history ring update. fill3: all three frames are the current one (reset,
-// soccer_env.py:90-96). Only the current snapshot is written back (26 floats), into the
-// slot that held t-2.
-__device__ __forceinline__ void emit_frames(const DevState& S, const Params& P, int64_t e, Env& E, bool fill3,
-                                            const Snap& s2_in, const Snap& s1_in, float* __restrict__ obs) {
-  Snap s0;
-  snap_of(E, s0);
-  const int head = (E.meta & META_RING) ? 1 : 0;  // slot holding t-1; the other holds t-2
-  const Snap& s2 = fill3 ? s0 : s2_in;
-  const Snap& s1 = fill3 ? s0 : s1_in;
+#ifndef MS_OBS_AGENT_MAJOR
+#define MS_OBS_AGENT_MAJOR 0  // 1: all three frames of agent 0, then agent 1, ... (variant switch)
+#endif
+// Frames t-2, t-1, t of every agent. Agent-major order finishes each 264-B row segment of an
+// agent in one burst of stores.
+__device__ __forceinline__ void emit_three(const Params& P, const Snap& s2, const Snap& s1, const Snap& s0,
+                                           float* __restrict__ row0) {
+  if (MS_OBS_AGENT_MAJOR && frame_inputs_in_range(P, s2) && frame_inputs_in_range(P, s1) &&
+      frame_inputs_in_range(P, s0)) {
+    float a2[6][3], a1[6][3], a0[6][3];
+    pair_vectors<true>(s2, a2);
+    pair_vectors<true>(s1, a1);
+    pair_vectors<true>(s0, a0);
+    static_for<0, 4>([&](auto ac) __attribute__((always_inline)) {
+      constexpr int A = decltype(ac)::value;
+      agent_frame_store<true, A, 0>(P, s2, a2, row0);
+      agent_frame_store<true, A, 1>(P, s1, a1, row0);
+      agent_frame_store<true, A, 2>(P, s0, a0, row0);
+    });
+  } else {
+    emit_snapshot<0>(P, s2, row0);
+    emit_snapshot<1>(P, s1, row0);
+    emit_snapshot<2>(P, s0, row0);
+  }
+}
+
+// Frames of a reset (soccer_env.py:90-96): all three stacked frames are the current one, and
+// the history slot (t-2 for the next step) is the current snapshot too.
+__device__ __forceinline__ void emit_fill3(const DevState& S, const Params& P, int64_t e, const Snap& s0,
+                                           float* __restrict__ obs) {
   if (obs && MS_ABLATE != 3) {
     float* dst = obs + e * 264;
-    emit_snapshot<0>(P, s2, dst);
-    emit_snapshot<1>(P, s1, dst);
+    emit_snapshot<0>(P, s0, dst);
+    emit_snapshot<1>(P, s0, dst);
     emit_snapshot<2>(P, s0, dst);
   }
-  if (fill3) {
-    snap_store(S, e, 0, s0);
-    snap_store(S, e, 1, s0);
-    E.meta &= ~(META_HE | META_RING);
-  } else {
-    snap_store(S, e, head ^ 1, s0);  // new t-1
-    E.meta ^= META_RING;
-  }
+  snap_store(S, e, s0);
 }
 
 // Game.reset (game.py:76-118): fresh bodies, score/steps 0, arbiters dropped, spawn.
@@ -390,16 +436,9 @@ struct CSlot {
 #endif
 #define MAXC (2 * MAXA)                 // contact capacity (2 per arbiter)
 
-__device__ __forceinline__ float cache_field(const DevState& S, int par, int k, int f, int64_t e) {
-  return S.CJ[((int64_t)(par * MAXA + k) * 4 + f) * S.n + e];
-}
-__device__ __forceinline__ void cache_write(const DevState& S, int par, int k, int64_t e, uint32_t hdr, float j0,
-                                            float j1, float j2, float j3) {
+__device__ __forceinline__ void cache_write(const DevState& S, int par, int k, int64_t e, uint32_t hdr, float4 j) {
   S.CH[(int64_t)(par * MAXA + k) * S.n + e] = hdr;
-  S.CJ[((int64_t)(par * MAXA + k) * 4 + 0) * S.n + e] = j0;
-  S.CJ[((int64_t)(par * MAXA + k) * 4 + 1) * S.n + e] = j1;
-  S.CJ[((int64_t)(par * MAXA + k) * 4 + 2) * S.n + e] = j2;
-  S.CJ[((int64_t)(par * MAXA + k) * 4 + 3) * S.n + e] = j3;
+  S.CJ[(int64_t)(par * MAXA + k) * S.n + e] = j;
 }
 
 // Per-lane working set of the contact pipeline.
@@ -526,32 +565,44 @@ __device__ __forceinline__ void lds_box(const Lds& L, int i, int lane, Box& b) {
 }
 
 // Old-cache cursor: the previous step's arbiter cache (sorted by pair id) is streamed once,
-// merged with this step's touched arbiters into the other (ping-pong) buffer.
+// merged with this step's touched arbiters into the other (ping-pong) buffer. Entries below KC
+// come from LDS (staged at kernel start), the rest from HBM.
 struct CacheWalk {
   int par, nc_old, cur, out;
   uint32_t curh;
 };
 
-__device__ __forceinline__ void cache_advance(const DevState& S, int64_t e, CacheWalk& W) {
+// (the HBM fallback is an explicit global load: a plain select between the LDS and the global
+// element lets the optimizer form one flat-address load)
+__device__ __forceinline__ uint32_t old_hdr(const DevState& S, const Lds& L, int lane, int64_t e, int par, int k) {
+  if (k < KC) return L.ch[k][lane];
+  return __builtin_nontemporal_load(&S.CH[(int64_t)(par * MAXA + k) * S.n + e]);
+}
+__device__ __forceinline__ float4 old_imp(const DevState& S, const Lds& L, int lane, int64_t e, int par, int k) {
+  if (k < KC) return L.cj[k][lane];
+  const float* g = (const float*)&S.CJ[(int64_t)(par * MAXA + k) * S.n + e];
+  return make_float4(__builtin_nontemporal_load(g), __builtin_nontemporal_load(g + 1), __builtin_nontemporal_load(g + 2),
+                     __builtin_nontemporal_load(g + 3));
+}
+
+__device__ __forceinline__ void cache_advance(const DevState& S, const Lds& L, int lane, int64_t e, CacheWalk& W) {
   ++W.cur;
-  W.curh = W.cur < W.nc_old ? S.CH[(int64_t)(W.par * MAXA + W.cur) * S.n + e] : 0xffffffffu;
+  W.curh = W.cur < W.nc_old ? old_hdr(S, L, lane, e, W.par, W.cur) : 0xffffffffu;
 }
 
 // emit the old entry under the cursor aged by one step (dropped at idle 3, cpSpaceArbiterSetFilter)
-__device__ __forceinline__ void cache_age_current(const DevState& S, int64_t e, CacheWalk& W,
+__device__ __forceinline__ void cache_age_current(const DevState& S, const Lds& L, int lane, int64_t e, CacheWalk& W,
                                                   unsigned long long* overflow_acc) {
   const uint32_t idle = ((W.curh >> 8) & 3u) + 1u;
   if (idle < 3u) {
     if (W.out < MAXA) {
-      cache_write(S, W.par ^ 1, W.out, e, (W.curh & ~(3u << 8)) | (idle << 8), cache_field(S, W.par, W.cur, 0, e),
-                  cache_field(S, W.par, W.cur, 1, e), cache_field(S, W.par, W.cur, 2, e),
-                  cache_field(S, W.par, W.cur, 3, e));
+      cache_write(S, W.par ^ 1, W.out, e, (W.curh & ~(3u << 8)) | (idle << 8), old_imp(S, L, lane, e, W.par, W.cur));
       ++W.out;
     } else {
       (*overflow_acc)++;
     }
   }
-  cache_advance(S, e, W);
+  cache_advance(S, L, lane, e, W);
 }
 
 // cpSpaceCollideShapes + cpArbiterUpdate for one touching pair
@@ -559,14 +610,14 @@ __device__ __forceinline__ void add_arbiter(const DevState& S, int64_t e, const 
                                             CSlot* ovf, CacheWalk& W, int p, int ba, int bb, const Col& col, float u,
                                             unsigned long long* overflow_acc) {
   if (C.na >= MAXA) { (*overflow_acc)++; return; }
-  while (W.cur < W.nc_old && (int)(W.curh & 63u) < p) cache_age_current(S, e, W, overflow_acc);
+  while (W.cur < W.nc_old && (int)(W.curh & 63u) < p) cache_age_current(S, L, lane, e, W, overflow_acc);
   const bool found = W.cur < W.nc_old && (int)(W.curh & 63u) == p;
   const uint32_t oh = W.curh;
   float oj[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   if (found) {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) oj[f] = cache_field(S, W.par, W.cur, f, e);
-    cache_advance(S, e, W);
+    const float4 j = old_imp(S, L, lane, e, W.par, W.cur);
+    oj[0] = j.x; oj[1] = j.y; oj[2] = j.z; oj[3] = j.w;
+    cache_advance(S, L, lane, e, W);
   }
   int pos = W.out;
   if (W.out < MAXA) ++W.out; else { (*overflow_acc)++; pos = 63; }
@@ -602,7 +653,7 @@ __device__ __forceinline__ void write_arbiter_cache(const DevState& S, int npar,
   const bool two = CS_COUNT(c0.m) > 1;
   const uint32_t hdr = (uint32_t)CS_PAIR(c0.m) | (CS_COUNT(c0.m) << 6) | (CS_HASH(c0.m) << 16) |
                        ((two ? CS_HASH(c1.m) : 0u) << 24);
-  cache_write(S, npar, CS_POS(c0.m), e, hdr, c0.jn, c0.jt, two ? c1.jn : 0.0f, two ? c1.jt : 0.0f);
+  cache_write(S, npar, CS_POS(c0.m), e, hdr, make_float4(c0.jn, c0.jt, two ? c1.jn : 0.0f, two ? c1.jt : 0.0f));
 }
 
 #define FOR_CONTACTS(C, OVF, BODY)                                    \
@@ -692,7 +743,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
 #endif
   W.cur = 0;
   W.out = 0;
-  W.curh = W.nc_old > 0 ? S.CH[(int64_t)(W.par * MAXA + 0) * S.n + e] : 0xffffffffu;
+  W.curh = W.nc_old > 0 ? old_hdr(S, L, lane, e, W.par, 0) : 0xffffffffu;
 
   // narrowphase, one compacted loop per pair class so each lane visits only its own touching
   // pairs; class order + ctz order = canonical pair order (DESIGN.md pair table)
@@ -738,7 +789,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     col_circle_seg(ballc, BR, sg, col);
     if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, 42 + s, 4, 5, col, P.u_bw, overflow_acc);
   }
-  while (W.cur < W.nc_old) cache_age_current(S, e, W, overflow_acc);
+  while (W.cur < W.nc_old) cache_age_current(S, L, lane, e, W, overflow_acc);
   STAMP(3);
 #ifdef MS_STAMPS
   {
@@ -809,26 +860,58 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
 }
 
 // ---- kernels ---------------------------------------------------------------------------------
-__device__ __forceinline__ void load_scalars(const DevState& S, int64_t e, Env& E) {
-  const int64_t n = S.n;
-  E.steps = S.I[I_STEPS * n + e];
-  const uint32_t sc = (uint32_t)S.I[I_SCORE * n + e];
-  E.score_blue = (int)(sc & 0xffffu);
-  E.score_red = (int)(sc >> 16);
-  E.meta = (uint32_t)S.I[I_META * n + e];
+__device__ __forceinline__ void unpack_scalars(int4 v, Env& E) {
+  E.steps = v.x;
+  E.score_blue = (int)((uint32_t)v.y & 0xffffu);
+  E.score_red = (int)((uint32_t)v.y >> 16);
+  E.meta = (uint32_t)v.z;
+  E.rng.u32 = (uint32_t)v.w;
 }
+__device__ __forceinline__ void load_scalars(const DevState& S, int64_t e, Env& E) { unpack_scalars(S.I4[e], E); }
 __device__ __forceinline__ void store_scalars(const DevState& S, int64_t e, const Env& E) {
-  const int64_t n = S.n;
-  S.I[I_STEPS * n + e] = E.steps;
-  S.I[I_SCORE * n + e] = (int32_t)(((uint32_t)E.score_blue & 0xffffu) | ((uint32_t)E.score_red << 16));
-  S.I[I_META * n + e] = (int32_t)E.meta;
+  S.I4[e] = make_int4(E.steps, (int32_t)(((uint32_t)E.score_blue & 0xffffu) | ((uint32_t)E.score_red << 16)),
+                      (int32_t)E.meta, (int32_t)E.rng.u32);
 }
 
-__global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P, const float* __restrict__ actions,
-                                                           float* __restrict__ obs, float* __restrict__ rew,
-                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                           int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
-                                                           Counters* ctr) {
+// One env.step of every env (SoccerEnv.step -> Game.step, soccer_env.py:100-154,
+// game/game.py:378-437). Order inside a lane:
+//   1. every HBM read of the step is issued up front: scalars, bodies, the t-2 snapshot,
+//      actions, the old arbiter cache (entries < KC) and, when a respawn is possible, PCG64;
+//   2. frames t-2 (snapshot) and t-1 (the body state before this step IS the t-1 snapshot) of
+//      the stacked obs are emitted and the history slot is rewritten with the t-1 snapshot, so
+//      2/3 of the obs stores drain while the physics runs;
+//   3. physics, goal, rewards, outputs, resets with no further HBM reads (gfx9 has one vmcnt
+//      for loads and stores, so a read after those stores would wait for them);
+//   4. frame t and the state stores. A lane whose stack is refilled (first step after a
+//      reset, or a vec auto-reset this step) writes all three frames and the slot here.
+// The reference's default config.json physics and rewards (make_params of ms_config_default,
+// bit for bit; ms_create compares the two and launches the specialised step kernel only when
+// they are identical). As compile-time constants the masses, restitution/friction products,
+// reward multipliers and the segment table fold into the instructions that use them.
+__host__ __device__ constexpr Params default_params() {
+  return Params{
+    0x1.111112p-6f, 0x1.99999ap-4f, 0x1.99999ap-4f,
+    {0x1.99999ap-4f, 0x1.99999ap-4f, 0x1.99999ap-4f, 0x1.99999ap-4f, 0x1p+0f, 0.0f},
+    {0x1.47ae14p-7f, 0x1.47ae14p-7f, 0x1.47ae14p-7f, 0x1.47ae14p-7f, 0x1.99999ap-4f, 0.0f},
+    0x1.fae148p-1f, 0x1.f0a3d8p-1f, 200.0f, 150000.0f, 1000.0f, 200.0f, 10.0f,
+    0x1.47ae16p-5f, 0x1.47ae16p-1f, 0x1.851eb8p-3f, 0x1.47ae16p-3f, 0x1.851eb8p-3f, 0x1.47ae16p-3f,
+    0x1.851eb8p-3f, 0.0f, 0x1.ce147ap-1f, 0x1.47ae16p-5f,
+    0x1.0624dep-9f, 0x1.99999ap-4f, 0x1.4f8b58p-17f, 4.0f, 0.0f, 0.0f,
+    1000, 1, 1,
+    {{10.0f, 10.0f, 790.0f, 10.0f, -0.0f, 1.0f, 2.0f, {8.0f, 8.0f, 792.0f, 12.0f}},
+     {10.0f, 590.0f, 790.0f, 590.0f, -0.0f, 1.0f, 2.0f, {8.0f, 588.0f, 792.0f, 592.0f}},
+     {10.0f, 10.0f, 10.0f, 225.0f, -1.0f, 0.0f, 2.0f, {8.0f, 8.0f, 12.0f, 227.0f}},
+     {10.0f, 375.0f, 10.0f, 590.0f, -1.0f, 0.0f, 2.0f, {8.0f, 373.0f, 12.0f, 592.0f}},
+     {790.0f, 10.0f, 790.0f, 225.0f, -1.0f, 0.0f, 2.0f, {788.0f, 8.0f, 792.0f, 227.0f}},
+     {790.0f, 375.0f, 790.0f, 590.0f, -1.0f, 0.0f, 2.0f, {788.0f, 373.0f, 792.0f, 592.0f}},
+     {10.0f, 225.0f, 10.0f, 375.0f, -1.0f, 0.0f, 1.0f, {9.0f, 224.0f, 11.0f, 376.0f}},
+     {790.0f, 225.0f, 790.0f, 375.0f, -1.0f, 0.0f, 1.0f, {789.0f, 224.0f, 791.0f, 376.0f}}}};
+}
+__device__ __forceinline__ void step_envs(const DevState& S, const Params& P, const float* __restrict__ actions,
+                                          float* __restrict__ obs, float* __restrict__ rew,
+                                          uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                          int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
+                                          Counters* ctr) {
   __shared__ Lds L;
   STAMP(0);
   const int lane = threadIdx.x;
@@ -836,21 +919,52 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
   const int64_t e = e0 + lane;
   bool active = e < S.n;
 
-  // SoccerEnv.step validation + clip + fp32 scaling (soccer_env.py:101-125)
-  // the actions, scalars and bodies are loaded together: one memory round trip before physics
-  float a[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) a[k] = 0.0f;
+  // (1) loads, in the order their data is needed. They are unconditional (an inactive lane
+  // reads env n-1): loads under a lane branch make the compiler copy the loaded registers at
+  // the join, and every copy waits for its load.
+  const int64_t el = active ? e : S.n - 1;
   Env E;
-  if (active) {
-    const float4* ap = (const float4*)(actions + e * 12);
+  unpack_scalars(S.I4[el], E);
+  load_bodies(S, el, E);
+  Snap h2;  // obs-history snapshot t-2
+  snap_load(S, el, h2);
+  float a[12];
+  {
+    const float4* ap = (const float4*)(actions + el * 12);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      float4 v = ap[q];
+      const float4 v = ap[q];
       a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
     }
-    load_scalars(S, e, E);
-    load_bodies(S, e, E);
+  }
+  int nco = META_NC(E.meta);
+  const int par0 = (E.meta & META_PAR) ? 1 : 0;
+#if MS_ABLATE == 4  // old arbiter cache ignored (timing ablation)
+  nco = 0;
+#endif
+  // old arbiter cache entries k < KC. No branch (so the compiler's wait counts stay exact): a
+  // lane without entry k re-reads its own scalars/bodies, which are in L1, instead.
+  uint32_t pch[KC];
+  float4 pcj[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const bool need = k < nco;
+    const int64_t o = (int64_t)(par0 * MAXA + k) * S.n + el;
+    const uint32_t* hp = need ? &S.CH[o] : (const uint32_t*)&S.I4[el];
+    const float4* jp = need ? &S.CJ[o] : &S.B4[el];
+    pch[k] = *hp;
+    pcj[k] = *jp;
+  }
+#pragma unroll
+  for (int k = 0; k < KC; ++k) { L.ch[k][lane] = pch[k]; L.cj[k][lane] = pcj[k]; }
+  stage_segments(P, L, lane);
+  bool fill3 = false, rng_loaded = false, rng_dirty = false;
+  Snap h1;  // obs-history snapshot t-1: the body state before this step
+  // frames t-2 and t-1 before the physics (MS_EARLY_OBS 1: every block, 2: odd blocks) or with
+  // frame t at the end (0)
+  const bool early = MS_EARLY_OBS == 1 || (MS_EARLY_OBS == 2 && (blockIdx.x & 1));
+  if (active) {
+    // SoccerEnv.step validation (soccer_env.py:101-117): a non-finite action skips the env
     bool finite = true;
 #pragma unroll
     for (int k = 0; k < 12; ++k) finite = finite && isfinite(a[k]);
@@ -860,23 +974,34 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
       active = false;
     }
   }
-  stage_segments(P, L, lane);
-  Snap h2, h1;  // obs history snapshots t-2, t-1
+  if (active) {
+    E.steps += 1;
+    const bool done_now = P.max_steps > 0 && E.steps >= P.max_steps;
+    // PCG64 state now if this step may respawn (ball within 30 px of a goal mouth — it moves
+    // <= 4 px per step — or the episode ends here)
+    if (((E.px[4] < 40.0f || E.px[4] > 760.0f) && E.py[4] > 195.0f && E.py[4] < 405.0f) || (P.autoreset && done_now)) {
+      load_rng(S, e, E);
+      rng_loaded = true;
+    }
+    // (2) frames t-2 and t-1; the stack is refilled instead after a reset (hist_empty) or an
+    // auto-reset at the end of this step
+    fill3 = (E.meta & META_HE) != 0 || (P.autoreset && done_now);
+    snap_of(E, h1);
+    if (!fill3 && early) {
+      if (obs && MS_ABLATE != 3) {
+        float* dst = obs + e * 264;
+        emit_snapshot<0>(P, h2, dst);
+        emit_snapshot<1>(P, h1, dst);
+      }
+      snap_store(S, e, h1);  // t-1 becomes the next step's t-2
+    }
+  }
+
   float pvx[5], pvy[5];
-  bool fill3 = false, rng_dirty = false, rng_loaded = false;
   if (active) {
     float fx[4], fy[4], tq[4];
 #pragma unroll
     for (int b = 0; b < 5; ++b) { pvx[b] = E.px[b]; pvy[b] = E.py[b]; }
-    E.steps += 1;
-    // PCG64 state now if this step may respawn (ball within 30 px of a goal mouth — it moves
-    // ≤ 4 px per step — or the episode ends here): loaded at the end it is a dependent HBM
-    // read in the slowest waves, issued when the memory system is busiest
-    if (((E.px[4] < 40.0f || E.px[4] > 760.0f) && E.py[4] > 195.0f && E.py[4] < 405.0f) ||
-        (P.autoreset && P.max_steps > 0 && E.steps >= P.max_steps)) {
-      load_rng(S, e, E);
-      rng_loaded = true;
-    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float F[3];
@@ -897,17 +1022,6 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
     physics_step(S, P, e, E, fx, fy, tq, L, lane, &ovf);
     STAMP(7);
     if (ovf) atomicAdd(&ctr->overflow, ovf);
-    {  // history snapshots: issued here so their latency hides under the reward math
-      const int head = (E.meta & META_RING) ? 1 : 0;
-#if MS_ABLATE == 5  // history not loaded (timing ablation)
-      (void)head;
-      snap_of(E, h2);
-      snap_of(E, h1);
-#else
-      snap_load(S, e, head ^ 1, h2);
-      snap_load(S, e, head, h1);
-#endif
-    }
 
     // goal detection (game.py:401-412)
     int goal = 0;
@@ -930,24 +1044,49 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params P,
     if (goal_out) goal_out[e] = (int8_t)goal;
     if (score_out) *(int2*)(score_out + e * 2) = make_int2(E.score_blue, E.score_red);
 
-    fill3 = (E.meta & META_HE) != 0;
     if (done && P.autoreset) {
       // marl_vecenv.py:48-51: env.reset(options={"use_full_random_positions": True})
       if (!rng_dirty && !rng_loaded) load_rng(S, e, E);
       rng_dirty = true;
       reset_env_regs(E, MS_SPAWN_FULL_RANDOM);
-      fill3 = true;
     }
   }
   STAMP(8);
   if (active) {
-    emit_frames(S, P, e, E, fill3, h2, h1, obs);
+    // (4) frame t; refilled stacks get all three frames and the history slot
+    Snap s0;
+    snap_of(E, s0);
+    if (fill3) {
+      emit_fill3(S, P, e, s0, obs);
+      E.meta &= ~META_HE;
+    } else if (early) {
+      if (obs && MS_ABLATE != 3) emit_snapshot<2>(P, s0, obs + e * 264);
+    } else {
+      if (obs && MS_ABLATE != 3) emit_three(P, h2, h1, s0, obs + e * 264);
+      snap_store(S, e, h1);  // t-1 becomes the next step's t-2
+    }
     STAMP(9);
     if (rng_dirty) store_rng(S, e, E);
     store_bodies(S, e, E);
     store_scalars(S, e, E);
   }
   STAMP(10);
+}
+
+template <bool DEFAULT_PARAMS>
+__global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params Pin, const float* __restrict__ actions,
+                                                           float* __restrict__ obs, float* __restrict__ rew,
+                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                           int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
+                                                           Counters* ctr) {
+  if constexpr (DEFAULT_PARAMS) {
+    Params Pd = default_params();
+    Pd.max_steps = Pin.max_steps;  // episode length and auto-reset stay runtime values
+    Pd.autoreset = Pin.autoreset;
+    step_envs(S, Pd, actions, obs, rew, term, trunc, goal_out, score_out, ctr);
+  } else {
+    step_envs(S, Pin, actions, obs, rew, term, trunc, goal_out, score_out, ctr);
+  }
 }
 
 __global__ __launch_bounds__(MS_BLOCK) void ms_reset_kernel(DevState S, Params P, const uint64_t* __restrict__ pcg,
@@ -957,25 +1096,23 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_reset_kernel(DevState S, Params P
   const bool active = e < S.n && (!mask || mask[e]);
   if (!active) return;
   Env E;
-  Snap h0;  // unused: fill3 frames come from the fresh state
-  {
-    load_scalars(S, e, E);
-    if (pcg) {
-      E.rng.shi = pcg[e * 4 + 0]; E.rng.slo = pcg[e * 4 + 1];
-      E.rng.ihi = pcg[e * 4 + 2]; E.rng.ilo = pcg[e * 4 + 3];
-      E.rng.has32 = 0; E.rng.u32 = 0;
-    } else {
-      load_rng(S, e, E);
-    }
-    reset_env_regs(E, mode);
+  load_scalars(S, e, E);
+  if (pcg) {
+    E.rng.shi = pcg[e * 4 + 0]; E.rng.slo = pcg[e * 4 + 1];
+    E.rng.ihi = pcg[e * 4 + 2]; E.rng.ilo = pcg[e * 4 + 3];
+    E.rng.has32 = 0; E.rng.u32 = 0;
+  } else {
+    load_rng(S, e, E);
   }
-  emit_frames(S, P, e, E, true, h0, h0, obs);
-  {
-    if (set_hist_empty) E.meta |= META_HE;
-    store_rng(S, e, E);
-    store_bodies(S, e, E);
-    store_scalars(S, e, E);
-  }
+  reset_env_regs(E, mode);
+  Snap s0;
+  snap_of(E, s0);
+  emit_fill3(S, P, e, s0, obs);
+  E.meta &= ~META_HE;
+  if (set_hist_empty) E.meta |= META_HE;
+  store_rng(S, e, E);
+  store_bodies(S, e, E);
+  store_scalars(S, e, E);
 }
 
 __global__ __launch_bounds__(MS_BLOCK) void ms_observe_kernel(DevState S, Params P, float* __restrict__ frames) {
@@ -996,7 +1133,6 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_observe_kernel(DevState S, Params
 __global__ void ms_export_kernel(DevState S, ms_env_state* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= S.n) return;
-  const int64_t n = S.n;
   Env E;
   load_scalars(S, e, E);
   load_bodies(S, e, E);
@@ -1008,10 +1144,16 @@ __global__ void ms_export_kernel(DevState S, ms_env_state* __restrict__ out) {
     d.angle = b < 4 ? E.ang[b < 4 ? b : 0] : 0.0f;
     d.w = E.w[b]; d.vbx = E.vbx[b]; d.vby = E.vby[b]; d.wb = E.wb[b];
   }
-  const int head = (E.meta & META_RING) ? 1 : 0;
-  for (int k = 0; k < MS_SNAP_SIZE; ++k) {
-    o.snap[0][k] = S.F[(int64_t)(F_SNAP + (head ^ 1) * MS_SNAP_SIZE + k) * n + e];
-    o.snap[1][k] = S.F[(int64_t)(F_SNAP + head * MS_SNAP_SIZE + k) * n + e];
+  Snap h2, h1;
+  snap_load(S, e, h2);
+  snap_of(E, h1);  // the t-1 snapshot is the current body state
+  for (int b = 0; b < 5; ++b) {
+    o.snap[0][b] = h2.px[b]; o.snap[0][5 + b] = h2.py[b];
+    o.snap[1][b] = h1.px[b]; o.snap[1][5 + b] = h1.py[b];
+  }
+  for (int i = 0; i < 4; ++i) {
+    o.snap[0][10 + i] = h2.vx[i]; o.snap[0][14 + i] = h2.vy[i]; o.snap[0][18 + i] = h2.ang[i]; o.snap[0][22 + i] = h2.w[i];
+    o.snap[1][10 + i] = h1.vx[i]; o.snap[1][14 + i] = h1.vy[i]; o.snap[1][18 + i] = h1.ang[i]; o.snap[1][22 + i] = h1.w[i];
   }
   o.steps = E.steps; o.score_blue = E.score_blue; o.score_red = E.score_red;
   o.mode = (uint8_t)META_MODE(E.meta);
@@ -1028,18 +1170,19 @@ __global__ void ms_export_kernel(DevState S, ms_env_state* __restrict__ out) {
     ms_arbiter_state& A = o.arb[k];
     memset(&A, 0, sizeof(A));
     if (k >= nc) continue;
-    const uint32_t h = S.CH[(int64_t)(par * MAXA + k) * n + e];
+    const uint32_t h = S.CH[(int64_t)(par * MAXA + k) * S.n + e];
     A.pair = h & 63u; A.count = (h >> 6) & 3u; A.idle = (h >> 8) & 3u;
     A.hash[0] = (h >> 16) & 0xffu; A.hash[1] = (h >> 24) & 0xffu;
-    A.jn[0] = cache_field(S, par, k, 0, e); A.jt[0] = cache_field(S, par, k, 1, e);
-    A.jn[1] = cache_field(S, par, k, 2, e); A.jt[1] = cache_field(S, par, k, 3, e);
+    const float4 j = S.CJ[(int64_t)(par * MAXA + k) * S.n + e];
+    A.jn[0] = j.x; A.jt[0] = j.y; A.jn[1] = j.z; A.jt[1] = j.w;
   }
 }
 
+// snap[1] (t-1) is not stored: it is the body state itself, which every state the library or
+// the oracle exports satisfies.
 __global__ void ms_import_kernel(DevState S, const ms_env_state* __restrict__ in) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= S.n) return;
-  const int64_t n = S.n;
   const ms_env_state& o = in[e];
   Env E;
   for (int b = 0; b < 5; ++b) {
@@ -1053,19 +1196,17 @@ __global__ void ms_import_kernel(DevState S, const ms_env_state* __restrict__ in
   E.meta = (uint32_t)(o.mode & 3) | (o.hist_empty ? META_HE : 0u) | ((uint32_t)nc << 8) | (o.has_uint32 ? META_H32 : 0u);
   E.rng.shi = o.pcg_state_hi; E.rng.slo = o.pcg_state_lo; E.rng.ihi = o.pcg_inc_hi; E.rng.ilo = o.pcg_inc_lo;
   E.rng.has32 = o.has_uint32; E.rng.u32 = o.uinteger;
-  for (int k = 0; k < MS_SNAP_SIZE; ++k) {  // ring head = 1
-    S.F[(int64_t)(F_SNAP + 0 * MS_SNAP_SIZE + k) * n + e] = o.snap[0][k];
-    S.F[(int64_t)(F_SNAP + 1 * MS_SNAP_SIZE + k) * n + e] = o.snap[1][k];
+  Snap h2;
+  for (int b = 0; b < 5; ++b) { h2.px[b] = o.snap[0][b]; h2.py[b] = o.snap[0][5 + b]; }
+  for (int i = 0; i < 4; ++i) {
+    h2.vx[i] = o.snap[0][10 + i]; h2.vy[i] = o.snap[0][14 + i]; h2.ang[i] = o.snap[0][18 + i]; h2.w[i] = o.snap[0][22 + i];
   }
-  E.meta |= META_RING;
+  snap_store(S, e, h2);
   for (int k = 0; k < nc; ++k) {
     const ms_arbiter_state& A = o.arb[k];
-    S.CH[(int64_t)k * n + e] = (uint32_t)(A.pair & 63u) | ((uint32_t)(A.count & 3u) << 6) | ((uint32_t)(A.idle & 3u) << 8) |
-                               ((uint32_t)A.hash[0] << 16) | ((uint32_t)A.hash[1] << 24);
-    S.CJ[((int64_t)k * 4 + 0) * n + e] = A.jn[0];
-    S.CJ[((int64_t)k * 4 + 1) * n + e] = A.jt[0];
-    S.CJ[((int64_t)k * 4 + 2) * n + e] = A.jn[1];
-    S.CJ[((int64_t)k * 4 + 3) * n + e] = A.jt[1];
+    S.CH[(int64_t)k * S.n + e] = (uint32_t)(A.pair & 63u) | ((uint32_t)(A.count & 3u) << 6) |
+                                 ((uint32_t)(A.idle & 3u) << 8) | ((uint32_t)A.hash[0] << 16) | ((uint32_t)A.hash[1] << 24);
+    S.CJ[(int64_t)k * S.n + e] = make_float4(A.jn[0], A.jt[0], A.jn[1], A.jt[1]);
   }
   store_rng(S, e, E);
   store_bodies(S, e, E);
@@ -1095,6 +1236,7 @@ struct ms_env {
   hipStream_t stream;
   int64_t n;
   Params P;
+  bool default_params;  // P == default_params() up to max_steps/autoreset: specialised kernel
   DevState S;
   void* mem;
   Counters* ctr;
@@ -1251,6 +1393,21 @@ static void make_params(const ms_config* cfg, Params* P) {
   }
 }
 
+// P equals the compile-time default_params() bit for bit, apart from the runtime fields
+static bool params_are_default(const Params& P) {
+  Params d = default_params();
+  d.max_steps = P.max_steps;
+  d.autoreset = P.autoreset;
+  return memcmp(&d, &P, sizeof(Params)) == 0;
+}
+
+int ms_config_specialised(const ms_config* cfg) {
+  if (!cfg) return fail(MS_ERR_INVALID_ARGUMENT, "ms_config_specialised: null config") * -1;
+  Params P;
+  make_params(cfg, &P);
+  return params_are_default(P) ? 1 : 0;
+}
+
 static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 
 int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms_env** out) {
@@ -1266,24 +1423,27 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
   h->n = n_envs;
   if (cfg) h->cfg = *cfg; else ms_config_default(&h->cfg);
   make_params(&h->cfg, &h->P);
+  h->default_params = params_are_default(h->P);
   const size_t n = (size_t)n_envs;
-  const size_t bytes_F = sizeof(float) * PL_F * n;
-  const size_t bytes_I = sizeof(int32_t) * PL_I * n;
-  const size_t bytes_R = sizeof(uint64_t) * 4 * n;
+  const size_t bytes_B = sizeof(float4) * G_BODY * n;
+  const size_t bytes_H = sizeof(float4) * G_SNAP * n;
+  const size_t bytes_I = sizeof(int4) * n;
+  const size_t bytes_R = sizeof(ulonglong2) * 2 * n;
   const size_t bytes_CH = sizeof(uint32_t) * 2 * MAXA * n;
-  const size_t bytes_CJ = sizeof(float) * 2 * MAXA * 4 * n;
-  const size_t total = bytes_R + bytes_F + bytes_I + bytes_CH + bytes_CJ + 256;
+  const size_t bytes_CJ = sizeof(float4) * 2 * MAXA * n;
+  const size_t total = bytes_R + bytes_B + bytes_H + bytes_I + bytes_CJ + bytes_CH + 256;
   char* base = nullptr;
   if (hipMalloc((void**)&base, total) != hipSuccess) {
     delete h;
     return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of device state failed");
   }
   h->mem = base;
-  h->S.R = (uint64_t*)base; base += bytes_R;
-  h->S.F = (float*)base; base += bytes_F;
-  h->S.I = (int32_t*)base; base += bytes_I;
+  h->S.R2 = (ulonglong2*)base; base += bytes_R;
+  h->S.B4 = (float4*)base; base += bytes_B;
+  h->S.H4 = (float4*)base; base += bytes_H;
+  h->S.I4 = (int4*)base; base += bytes_I;
+  h->S.CJ = (float4*)base; base += bytes_CJ;
   h->S.CH = (uint32_t*)base; base += bytes_CH;
-  h->S.CJ = (float*)base; base += bytes_CJ;
   h->S.n = n_envs;
   h->S.stamps = nullptr;
   // contact-slot spill for pile-ups beyond KREG contacts: reserved address space, touched
@@ -1365,8 +1525,12 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
   if (((uintptr_t)actions & 15u) || ((uintptr_t)obs & 7u) || ((uintptr_t)rew & 15u) || ((uintptr_t)term & 3u) ||
       ((uintptr_t)trunc & 3u) || ((uintptr_t)score & 7u))
     return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: misaligned buffer (actions/rew 16 B, obs/score 8 B, flags 4 B)");
-  hipLaunchKernelGGL(ms_step_kernel, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S, h->P,
-                     actions, obs, rew, term, trunc, goal, score, h->ctr);
+  if (h->default_params)
+    hipLaunchKernelGGL(ms_step_kernel<true>, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S, h->P,
+                       actions, obs, rew, term, trunc, goal, score, h->ctr);
+  else
+    hipLaunchKernelGGL(ms_step_kernel<false>, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S,
+                       h->P, actions, obs, rew, term, trunc, goal, score, h->ctr);
   HIPCHK(hipGetLastError());
   return MS_OK;
 }

@@ -61,6 +61,7 @@ EXPORTED = (
     "ms_config_default", "ms_create", "ms_destroy", "ms_set_stream", "ms_num_envs", "ms_seed_pcg64",
     "ms_seed_pcg64_range", "ms_reset", "ms_step", "ms_observe", "ms_export_state", "ms_import_state",
     "ms_debug_rewards", "ms_get_stats", "ms_reset_stats", "ms_last_error", "ms_abi_version",
+    "ms_config_specialised",
 )
 
 _lib = None
@@ -104,6 +105,9 @@ def lib():
     L.ms_reset_stats.argtypes = [P]
     L.ms_last_error.restype = C.c_char_p
     L.ms_abi_version.restype = C.c_int
+    if hasattr(L, "ms_config_specialised"):  # absent only in older builds timed by tools/variants.py
+        L.ms_config_specialised.argtypes = [C.POINTER(MsConfig)]
+        L.ms_config_specialised.restype = C.c_int
     for fn in ("ms_create", "ms_destroy", "ms_set_stream", "ms_seed_pcg64", "ms_seed_pcg64_range", "ms_reset",
                "ms_step", "ms_observe", "ms_export_state", "ms_import_state", "ms_debug_rewards",
                "ms_get_stats", "ms_reset_stats"):
@@ -127,6 +131,15 @@ def default_config() -> MsConfig:
     cfg = MsConfig()
     lib().ms_config_default(C.byref(cfg))
     return cfg
+
+
+def config_specialised(cfg: MsConfig) -> bool:
+    """True when `cfg` runs the step kernel specialised for the reference's default physics
+    and rewards (compile-time constants); False: the generic kernel. Same results either way."""
+    rc = lib().ms_config_specialised(C.byref(cfg))
+    if rc < 0:
+        check(-rc, "ms_config_specialised")
+    return rc == 1
 
 
 def _seed_words(seed: int) -> np.ndarray:

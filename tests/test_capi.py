@@ -42,6 +42,25 @@ def test_abi_version_and_config_defaults():
     assert c.autoreset == 1
 
 
+def test_default_config_selects_specialised_step_kernel():
+    """ms_create launches the constant-folded step kernel only for parameters equal, bit for
+    bit, to the reference's defaults (max_steps/autoreset excepted); anything else runs the
+    generic kernel."""
+    from marlsoccer import _native as N
+    from marlsoccer.config import load_config, to_ms_config
+    assert N.config_specialised(N.default_config())
+    cfg = load_config()
+    assert N.config_specialised(to_ms_config(cfg, True))
+    assert N.config_specialised(to_ms_config(cfg, False))
+    cfg["simulation"]["max_steps"] = 70
+    assert N.config_specialised(to_ms_config(cfg, True))
+    for sect, key, val in (("rewards", "score_difference_multiplier", 5.0), ("rewards", "goal_conceded_penalty", 1.0),
+                           ("physics", "ball_mass", 2.0), ("physics", "max_velocity", 150.0)):
+        c = load_config()
+        c[sect][key] = val
+        assert not N.config_specialised(to_ms_config(c, True)), key
+
+
 @pytest.mark.parametrize("seed", [0, 1, 19, 123456, 2 ** 32 - 1, 2 ** 32, 2 ** 40 + 7, 2 ** 64 - 1, 2 ** 70 + 3])
 def test_seed_sequence_matches_numpy(seed):
     from marlsoccer import _native as N

@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""Per-phase wave timeline of ms_step_kernel (diagnostic; not part of the product path).
+
+    python tools/stamps.py --build            # here: hipcc -DMS_STAMPS -> lib/libmarlsoccer_stamps.so
+    python tools/stamps.py [--envs N] [--steps K] [--every M]   # on the GPU box
+
+The stamps build writes s_memtime at the STAMP(k) points of ms_env.hip into a
+[wave][16] buffer. For every M-th launch of a K-step episode this tool reads the buffer
+and reports, per phase, the mean cycles over all waves and over the slowest 5 % of waves
+(the ones that set the launch time), plus the launch span in cycles.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "marl-soccer_amd")
+STAMP_LIB = os.path.join(PKG, "lib", "libmarlsoccer_stamps.so")
+
+# (label, from, to) in kernel order; a stamp inside a branch no lane took is carried forward
+ORDER = [0, 1, 2, 11, 13, 3, 14, 4, 15, 5, 6, 7, 8, 9, 10]
+LABELS = {1: "load+actions", 2: "integrate+transforms", 11: "bp+nphase AA/BA", 13: "nphase static-agent",
+          3: "nphase ball-wall+cache age", 14: "prestep", 4: "velocity", 15: "warm start", 5: "solver x10",
+          6: "cache write", 7: "meta", 8: "goal+reward+outputs", 9: "obs frames+snap", 10: "state stores"}
+
+
+def build(extra=()):
+    import build_native
+    os.makedirs(os.path.dirname(STAMP_LIB), exist_ok=True)
+    cmd = [build_native.hipcc(), *build_native.FLAGS, "-DMS_STAMPS", *extra, "-o", STAMP_LIB, *build_native.SOURCES]
+    print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--every", type=int, default=10)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    sys.path.insert(0, PKG)
+    if a.build:
+        build()
+        return
+    os.environ["MARL_SOCCER_LIB"] = STAMP_LIB
+    import numpy as np
+    import torch
+    from marlsoccer import SoccerBatch, _native
+
+    L = _native.lib()
+    L.ms_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+    L.ms_debug_stamps.restype = C.c_int
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+    env = SoccerBatch(a.envs, device=0)
+    env.reset(seed=19)
+    ptr, nw = C.c_void_p(), C.c_int64()
+    L.ms_debug_stamps(env._h, C.byref(ptr), C.byref(nw))
+    nw = nw.value
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    acts = torch.empty((a.envs, 4, 3), device="cuda")
+    seg = {k: [] for k in ORDER[1:]}
+    seg_slow = {k: [] for k in ORDER[1:]}
+    spans, totals, slow_tot, maxnc = [], [], [], []
+    for t in range(a.steps):
+        acts.uniform_(-1.0, 1.0, generator=g)
+        sample = t % a.every == 0 and t > 0
+        if sample:
+            torch.cuda.synchronize()
+            hip.hipMemset(ptr, 0, nw * 16 * 8)
+            torch.cuda.synchronize()
+        env.step(acts)
+        if sample:
+            torch.cuda.synchronize()
+            buf = np.zeros((nw, 16), np.uint64)
+            hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+            hip.hipMemcpy(buf.ctypes.data, ptr, nw * 16 * 8, 2)
+            st = buf.astype(np.int64)
+            maxnc.append(st[:, 12].copy())
+            for i in range(1, len(ORDER)):  # carry forward stamps of untaken branches
+                k, prev = ORDER[i], ORDER[i - 1]
+                st[:, k] = np.where(st[:, k] == 0, st[:, prev], st[:, k])
+            tot = st[:, 10] - st[:, 0]
+            slow = tot >= np.quantile(tot, 0.95)
+            totals.append(tot.mean())
+            slow_tot.append(tot[slow].mean())
+            spans.append(st[:, 10].max() - st[:, 0].min())
+            for i in range(1, len(ORDER)):
+                d = st[:, ORDER[i]] - st[:, ORDER[i - 1]]
+                seg[ORDER[i]].append(d.mean())
+                seg_slow[ORDER[i]].append(d[slow].mean())
+    mnc = np.concatenate(maxnc)
+    res = {"envs": a.envs, "steps": a.steps, "samples": len(totals),
+           "wave_cycles_mean": float(np.mean(totals)), "wave_cycles_slowest5pct": float(np.mean(slow_tot)),
+           "launch_span_cycles": float(np.mean(spans)),
+           "max_contacts_per_wave": {str(int(v)): int((mnc == v).sum()) for v in np.unique(mnc)},
+           "phases": {LABELS[k]: {"mean": round(float(np.mean(seg[k])), 1),
+                                  "slow5": round(float(np.mean(seg_slow[k])), 1)} for k in ORDER[1:]}}
+    print(json.dumps(res, indent=1))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Build and time compile-time variants of the step kernel (diagnostic, not product code).
+
+    python tools/variants.py build NAME="-DFOO=1 -DBAR=2" ...   # here: lib/variants/lib_NAME.so
+    python tools/variants.py build-ref REV NAME                  # ms_env.hip of git REV
+    python tools/variants.py run [--envs N] [--steps K] NAME ...  # on the GPU box
+
+`run` times each variant with bench.py (MARL_SOCCER_LIB points the loader at the variant) in
+child processes, one after another, and prints one line per variant.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "marl-soccer_amd")
+VDIR = os.path.join(PKG, "lib", "variants")
+sys.path.insert(0, PKG)
+
+
+def build(name, defs, src=None):
+    import build_native
+    os.makedirs(VDIR, exist_ok=True)
+    out = os.path.join(VDIR, f"lib_{name}.so")
+    cmd = [build_native.hipcc(), *build_native.FLAGS, *defs.split(), "-o", out, src or build_native.SOURCES[0]]
+    subprocess.run(cmd, check=True)
+    print("built", out)
+
+
+def main():
+    a = sys.argv[1:]
+    if a[0] == "build":
+        for spec in a[1:]:
+            name, _, defs = spec.partition("=")
+            build(name, defs)
+    elif a[0] == "build-ref":
+        rev, name = a[1], a[2]
+        src = os.path.join(PKG, "csrc", f"_ref_{name}.hip")
+        with open(src, "w") as f:
+            f.write(subprocess.run(["git", "-C", ROOT, "show", f"{rev}:marl-soccer_amd/csrc/ms_env.hip"],
+                                   check=True, capture_output=True, text=True).stdout)
+        try:
+            build(name, "", src)
+        finally:
+            os.remove(src)
+    elif a[0] == "run":
+        envs, steps, names = "65536", "1000", []
+        i = 1
+        while i < len(a):
+            if a[i] == "--envs":
+                envs = a[i + 1]; i += 2
+            elif a[i] == "--steps":
+                steps = a[i + 1]; i += 2
+            else:
+                names.append(a[i]); i += 1
+        for name in names:
+            env = dict(os.environ, MARL_SOCCER_LIB=os.path.join(VDIR, f"lib_{name}.so"))
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--envs", envs,
+                                "--steps", steps], env=env, capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                print(name, "FAILED", r.stderr[-2000:], flush=True)
+                sys.exit(1)
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            print(f"{name:16s} {d['roofline']['kernel_ms'] * 1e3:8.2f} us/step  {d['value'] / 1e6:8.1f} M env-steps/s",
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
