@@ -123,6 +123,28 @@ __device__ __forceinline__ float div_nr(float n, float d, float r) {
   const float res = __builtin_fmaf(e, r, q);
   return n == 0.0f ? n : res;  // keeps the sign of a zero numerator
 }
+// div_nr of both components of a pair: the same operations per component as packed fp32
+// (v_pk_mul_f32 / v_pk_fma_f32)
+__device__ __forceinline__ V2 div_nr2(V2 n, float d, float r) {
+  const V2 nd = V2{-d, -d}, rv = V2{r, r};
+  V2 q = n * rv;
+  V2 e = __builtin_elementwise_fma(nd, q, n);
+  q = __builtin_elementwise_fma(e, rv, q);
+  e = __builtin_elementwise_fma(nd, q, n);
+  V2 res = __builtin_elementwise_fma(e, rv, q);
+  res.x = n.x == 0.0f ? n.x : res.x;
+  res.y = n.y == 0.0f ? n.y : res.y;
+  return res;
+}
+// div_nr for a numerator that is never -0: a +0 numerator gives +0 through the Newton steps
+// themselves (fma(-d, +0, +0) = +0 for d > 0), so the zero select is not needed
+__device__ __forceinline__ float div_nr_nonneg(float n, float d, float r) {
+  float q = n * r;
+  float e = __builtin_fmaf(-d, q, n);
+  q = __builtin_fmaf(e, r, q);
+  e = __builtin_fmaf(-d, q, n);
+  return __builtin_fmaf(e, r, q);
+}
 __device__ __forceinline__ float sqrt_nr(float x) {
   float s = __builtin_amdgcn_sqrtf(x);
   const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
@@ -507,8 +529,25 @@ __device__ __forceinline__ void spawn_positions(Rng& g, int mode, float px[5], f
 // ------------------------------------------------------------------------------------------
 // Observations: Game._get_observations (game.py:258-322) -> fp32 (soccer_env.py:131)
 // ------------------------------------------------------------------------------------------
+#ifndef MS_PK_OBS
+#define MS_PK_OBS 1
+#endif
 template <bool FAST = false>
 __device__ __forceinline__ void unit_mag(float dx, float dy, float* o) {
+  if constexpr (FAST && MS_PK_OBS) {
+    // x and y as one packed pair: d*d, the two quotients' Newton steps (div_nr per component)
+    const V2 d = v2(dx, dy);
+    const V2 d2 = d * d;
+    float mag = sqrt_nr(d2.x + d2.y);
+    const float r = rcp_nr(mag);
+    const bool big = mag > 1e-8f;
+    const V2 q = div_nr2(d, mag, r);
+    o[0] = big ? q.x : 0.0f;
+    o[1] = big ? q.y : 0.0f;
+    mag = big ? mag : 0.0f;
+    o[2] = div_nr_nonneg(mag, 1000.0f, rcp_nr(1000.0f));  // mag >= +0
+    return;
+  }
   if constexpr (FAST) {
     float mag = sqrt_nr(dx * dx + dy * dy);
     const float r = rcp_nr(mag);

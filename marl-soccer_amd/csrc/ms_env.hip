@@ -927,7 +927,7 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   unpack_scalars(S.I4[el], E);
   load_bodies(S, el, E);
   Snap h2;  // obs-history snapshot t-2
-  snap_load(S, el, h2);
+  if (MS_ABLATE != 6) snap_load(S, el, h2);
   float a[12];
   {
     const float4* ap = (const float4*)(actions + el * 12);
@@ -957,6 +957,7 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   }
 #pragma unroll
   for (int k = 0; k < KC; ++k) { L.ch[k][lane] = pch[k]; L.cj[k][lane] = pcj[k]; }
+
   stage_segments(P, L, lane);
   bool fill3 = false, rng_loaded = false, rng_dirty = false;
   Snap h1;  // obs-history snapshot t-1: the body state before this step
@@ -1061,6 +1062,8 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
       E.meta &= ~META_HE;
     } else if (early) {
       if (obs && MS_ABLATE != 3) emit_snapshot<2>(P, s0, obs + e * 264);
+    } else if (MS_ABLATE == 6) {  // frame t only, no history traffic (timing ablation)
+      if (obs) emit_snapshot<2>(P, s0, obs + e * 264);
     } else {
       if (obs && MS_ABLATE != 3) emit_three(P, h2, h1, s0, obs + e * 264);
       snap_store(S, e, h1);  // t-1 becomes the next step's t-2

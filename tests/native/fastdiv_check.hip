@@ -12,6 +12,8 @@
 using ms::rcp_nr;
 using ms::div_nr;
 using ms::sqrt_nr;
+using ms::div_nr2;
+using ms::div_nr_nonneg;
 __device__ __forceinline__ uint64_t mix(uint64_t z) { z += 0x9E3779B97F4A7C15ull; z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull; z = (z ^ (z >> 27)) * 0x94D049BB133111EBull; return z ^ (z >> 31); }
 __device__ float logu(uint64_t h, float lo_e, float hi_e) {  // log-uniform magnitude 2^[lo,hi) with random mantissa
   float e = lo_e + (hi_e - lo_e) * (float)(h & 0xffffff) / 16777216.0f;
@@ -30,7 +32,15 @@ __global__ void k(uint64_t base, unsigned long long* bad, unsigned long long* ba
   if (sel == 0) d = 200.0f; else if (sel == 1) d = 10.0f; else if (sel == 2) d = 1000.0f; else if (sel == 3) d = 3.1415927410125732f;
   else d = logu(h2, -28.0f, 14.0f);
   float q0 = n / d, q1 = div_nr(n, d, rcp_nr(d));
-  if (__float_as_uint(q0) != __float_as_uint(q1)) { unsigned long long c = atomicAdd(bad, 1ull); if (c < 4) { ex[4*c] = n; ex[4*c+1] = d; ex[4*c+2] = q0; ex[4*c+3] = q1; } }
+  // the packed pair form (second component: an independent numerator) and the +0-safe form
+  // must give the same bits as div_nr itself
+  const float n2 = (h2 & 2) ? -logu(h3 ^ h2, -100.0f, 30.0f) : ((h2 & 0x7c) == 0 ? 0.0f : logu(h3 ^ h2, -100.0f, 30.0f));
+  const ms::V2 qp = div_nr2(ms::V2{n, n2}, d, rcp_nr(d));
+  const float q2 = n2 / d;
+  bool wrong = __float_as_uint(qp.x) != __float_as_uint(q0) || __float_as_uint(qp.y) != __float_as_uint(q2);
+  const float na = fabsf(n);
+  wrong = wrong || __float_as_uint(div_nr_nonneg(na, d, rcp_nr(d))) != __float_as_uint(na / d);
+  if (wrong || __float_as_uint(q0) != __float_as_uint(q1)) { unsigned long long c = atomicAdd(bad, 1ull); if (c < 4) { ex[4*c] = n; ex[4*c+1] = d; ex[4*c+2] = q0; ex[4*c+3] = q1; } }
   // also dx/mag with mag = sqrt(dx^2+dy^2) structure
   float x = logu(h2 ^ h1, -90.0f, 126.0f);
   float s0 = sqrtf(x), s1 = sqrt_nr(x);
