@@ -334,7 +334,7 @@ __device__ __forceinline__ void emit_snapshot(const Params& P, const Snap& s, fl
 }
 
 #ifndef MS_OBS_AGENT_MAJOR
-#define MS_OBS_AGENT_MAJOR 0  // 1: all three frames of agent 0, then agent 1, ... (variant switch)
+#define MS_OBS_AGENT_MAJOR 1  // 0: frame-major order (t-2 of all agents, then t-1, then t)
 #endif
 // Frames t-2, t-1, t of every agent. Agent-major order finishes each 264-B row segment of an
 // agent in one burst of stores.

@@ -234,12 +234,13 @@ def test_actions_out_of_range_are_clipped(ms):
 
 # ---- full-size properties (BASELINE configs) ------------------------------------------------
 
-@pytest.mark.parametrize("n", [4096, 65536])
-def test_full_size_subsample_and_invariants(ms, n):
-    """Config 2/3 sizes: the 64-env subsample matches the fp32 oracle bit for bit, state stays
-    finite and inside the field, results are independent of the batch they run in."""
-    steps = 120
-    gpu = ms.SoccerBatch(n, config=cfg_dict(max_steps=50))
+@pytest.mark.parametrize("n,max_steps,steps", [(4096, 50, 120), (32768, 512, 560), (65536, 50, 120)])
+def test_full_size_subsample_and_invariants(ms, n, max_steps, steps):
+    """BASELINE config sizes: 4,096 and 65,536 envs per GPU (configs 2-4) and one GPU's shard of
+    config 5 (262,144 envs / 8 GPUs = 32,768, max_steps=512, default reward shaping, a whole
+    episode plus its auto-reset). The 64-env subsample matches the fp32 oracle bit for bit,
+    state stays finite and inside the field, results are independent of the batch they run in."""
+    gpu = ms.SoccerBatch(n, config=cfg_dict(max_steps=max_steps))
     gpu.reset(seed=19)
     sub = np.linspace(0, n - 1, 64).astype(np.int64)
     ref = orc.OracleBatch(64, "f32", oracle_cfg(gpu._cfg))
