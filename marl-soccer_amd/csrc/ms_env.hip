@@ -473,11 +473,15 @@ __device__ __forceinline__ float body_minv(const Params& P, int b) {
 __device__ __forceinline__ float body_iinv(const Params& P, int b) {
   return b < 4 ? P.i_inv[0] : (b == 4 ? P.i_inv[4] : 0.0f);
 }
+// shape b of an arbiter is never the ball (the ball is shape a of its agent pairs and of its
+// wall pairs, DESIGN.md pair table): an agent or the static body
+__device__ __forceinline__ float body_b_minv(const Params& P, int b) { return b < 4 ? P.m_inv[0] : 0.0f; }
+__device__ __forceinline__ float body_b_iinv(const Params& P, int b) { return b < 4 ? P.i_inv[0] : 0.0f; }
 
 // cpArbiterPreStep for one contact (velocities: previous step's post-solve values)
 __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds& L, int lane) {
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
-  const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_minv(P, bb), ib = body_iinv(P, bb);
+  const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_b_minv(P, bb), ib = body_b_iinv(P, bb);
   const int p = CS_PAIR(c.m);
   const float e_s = ((p - 10) & 7) < 6 ? P.e_aw : P.e_ag;
   const float e = p < 6 ? P.e_aa : (p < 10 ? P.e_ab : (p < 42 ? e_s : P.e_bw));
@@ -503,7 +507,7 @@ __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds
 __device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L, int lane) {
   if (!CS_WARM(c.m)) return;
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
-  const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_minv(P, bb), ib = body_iinv(P, bb);
+  const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_b_minv(P, bb), ib = body_b_iinv(P, bb);
   const V2 j = vrotate(c.n, v2(c.jn, c.jt));
   const V2 nj = vneg(j);
   L.ph.v[ba][lane] = L.ph.v[ba][lane] + vmult(nj, ma);
@@ -515,7 +519,7 @@ __device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L
 // cpArbiterApplyImpulse for one contact
 __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int lane) {
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
-  const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_minv(P, bb), ib = body_iinv(P, bb);
+  const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_b_minv(P, bb), ib = body_b_iinv(P, bb);
   const V2 n = c.n;
   const V2 r1 = c.r1, r2 = c.r2;
   const V2 vba = L.ph.vb[ba][lane], vbb = L.ph.vb[bb][lane];

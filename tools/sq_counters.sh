@@ -1,15 +1,15 @@
 #!/bin/bash
-# SQ/SQC counter passes over a short bench run (diagnostic). Each pass is its own run.
+# SQ counter passes over a short bench run (diagnostic). Each pass is its own run.
 # Usage: tools/sq_counters.sh <outdir> [bench args...]
 OUT=${1:-gpurun_out/sq}; shift
 mkdir -p $OUT
 export TMPDIR=/tmp
-rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS"
-P2="SQC_ICACHE_MISSES SQC_ICACHE_HITS"
-P3="SQ_IFETCH SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_WR"
+P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_VMEM SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SMEM"
+P3="SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL"
+P4="SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_CVT SQ_THREAD_CYCLES_VALU SQ_BUSY_CYCLES SQ_INSTS"
 i=0
-for P in "$P1" "$P2" "$P3"; do
+for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- python bench.py --steps 100 --warmup 20 --no-cpu-baseline "$@" > $OUT/p$i.log 2>&1
   rc=$?
