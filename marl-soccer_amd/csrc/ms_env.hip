@@ -151,6 +151,9 @@ enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
 #ifndef MS_EARLY_OBS
 #define MS_EARLY_OBS 0
 #endif
+#ifndef MS_LDS_VW
+#define MS_LDS_VW 1  // body velocity + angular velocity as one 16-B LDS record (0: split arrays)
+#endif
 #ifndef KC
 #define KC 4  // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (rare)
 #endif
@@ -159,16 +162,46 @@ struct Lds {
   Seg seg[8];  // static segments (walls, goal lines), read with per-lane indices
   struct {
     V2 p[6][MS_BLOCK];             // body position (body 5 = static, all 0)
+#if MS_LDS_VW
+    float4 vw[6][MS_BLOCK];        // velocity x, y, angular velocity (one 12-B access per body)
+    float4 bw[6][MS_BLOCK];        // bias velocity x, y, bias angular velocity
+#else
     V2 v[6][MS_BLOCK];             // velocity
     V2 vb[6][MS_BLOCK];            // bias velocity
     float w[6][MS_BLOCK];          // angular velocity
     float wb[6][MS_BLOCK];         // bias angular velocity
+#endif
     float box[BX_N][4][MS_BLOCK];  // agent box transform (p, cos, sin)
   } ph;
   // previous step's arbiter cache, entries 0..KC-1 (loaded with the state at kernel start)
   uint32_t ch[KC][MS_BLOCK];
   float4 cj[KC][MS_BLOCK];
 };
+
+// body velocity (v, w) and bias velocity (vb, wb) of body b in LDS
+#if MS_LDS_VW
+__device__ __forceinline__ void ld_v(const Lds& L, int b, int lane, V2& v, float& w) {
+  const float4 q = L.ph.vw[b][lane];
+  v = v2(q.x, q.y); w = q.z;
+}
+__device__ __forceinline__ void st_v(Lds& L, int b, int lane, V2 v, float w) {
+  float* d = (float*)&L.ph.vw[b][lane];
+  d[0] = v.x; d[1] = v.y; d[2] = w;
+}
+__device__ __forceinline__ void ld_vb(const Lds& L, int b, int lane, V2& v, float& w) {
+  const float4 q = L.ph.bw[b][lane];
+  v = v2(q.x, q.y); w = q.z;
+}
+__device__ __forceinline__ void st_vb(Lds& L, int b, int lane, V2 v, float w) {
+  float* d = (float*)&L.ph.bw[b][lane];
+  d[0] = v.x; d[1] = v.y; d[2] = w;
+}
+#else
+__device__ __forceinline__ void ld_v(const Lds& L, int b, int lane, V2& v, float& w) { v = L.ph.v[b][lane]; w = L.ph.w[b][lane]; }
+__device__ __forceinline__ void st_v(Lds& L, int b, int lane, V2 v, float w) { L.ph.v[b][lane] = v; L.ph.w[b][lane] = w; }
+__device__ __forceinline__ void ld_vb(const Lds& L, int b, int lane, V2& v, float& w) { v = L.ph.vb[b][lane]; w = L.ph.wb[b][lane]; }
+__device__ __forceinline__ void st_vb(Lds& L, int b, int lane, V2 v, float w) { L.ph.vb[b][lane] = v; L.ph.wb[b][lane] = w; }
+#endif
 
 // Compile-time loop: every reg[] access below uses a constant index from the first IR on,
 // so the slots are promoted to registers (an unrolled runtime loop is not: SROA runs first).
@@ -487,8 +520,10 @@ __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds
   const float e = p < 6 ? P.e_aa : (p < 10 ? P.e_ab : (p < 42 ? e_s : P.e_bw));
   const V2 n = c.n;
   const V2 body_delta = L.ph.p[bb][lane] - L.ph.p[ba][lane];
-  const V2 va = L.ph.v[ba][lane], vb = L.ph.v[bb][lane];
-  const float wa = L.ph.w[ba][lane], wbv = L.ph.w[bb][lane];
+  V2 va, vb;
+  float wa, wbv;
+  ld_v(L, ba, lane, va, wa);
+  ld_v(L, bb, lane, vb, wbv);
   const V2 r1 = c.r1, r2 = c.r2;
   const float rcn1 = vcross(r1, n), rcn2 = vcross(r2, n);
   c.nMass = 1.0f / ((ma + ia * rcn1 * rcn1) + (mb + ib * rcn2 * rcn2));
@@ -510,10 +545,12 @@ __device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L
   const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_b_minv(P, bb), ib = body_b_iinv(P, bb);
   const V2 j = vrotate(c.n, v2(c.jn, c.jt));
   const V2 nj = vneg(j);
-  L.ph.v[ba][lane] = L.ph.v[ba][lane] + vmult(nj, ma);
-  L.ph.w[ba][lane] += ia * vcross(c.r1, nj);
-  L.ph.v[bb][lane] = L.ph.v[bb][lane] + vmult(j, mb);
-  L.ph.w[bb][lane] += ib * vcross(c.r2, j);
+  V2 va, vb;
+  float wa, wbv;
+  ld_v(L, ba, lane, va, wa);
+  st_v(L, ba, lane, va + vmult(nj, ma), wa + ia * vcross(c.r1, nj));
+  ld_v(L, bb, lane, vb, wbv);
+  st_v(L, bb, lane, vb + vmult(j, mb), wbv + ib * vcross(c.r2, j));
 }
 
 // cpArbiterApplyImpulse for one contact
@@ -522,10 +559,12 @@ __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int
   const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_b_minv(P, bb), ib = body_b_iinv(P, bb);
   const V2 n = c.n;
   const V2 r1 = c.r1, r2 = c.r2;
-  const V2 vba = L.ph.vb[ba][lane], vbb = L.ph.vb[bb][lane];
-  const float wba = L.ph.wb[ba][lane], wbb = L.ph.wb[bb][lane];
-  const V2 va = L.ph.v[ba][lane], vb = L.ph.v[bb][lane];
-  const float wa = L.ph.w[ba][lane], wb_ = L.ph.w[bb][lane];
+  V2 vba, vbb, va, vb;
+  float wba, wbb, wa, wb_;
+  ld_vb(L, ba, lane, vba, wba);
+  ld_vb(L, bb, lane, vbb, wbb);
+  ld_v(L, ba, lane, va, wa);
+  ld_v(L, bb, lane, vb, wb_);
   const V2 vb1 = vadd(vba, vmult(vperp(r1), wba));
   const V2 vb2 = vadd(vbb, vmult(vperp(r2), wbb));
   const V2 vs1 = vadd(va, vmult(vperp(r1), wa));
@@ -554,14 +593,10 @@ __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int
   const V2 nj = vneg(j);
   // body a first, then body b (apply_bias_impulses then apply_impulses, cpArbiter.c);
   // a and b are distinct bodies, so the four updates commute per body.
-  L.ph.vb[ba][lane] = vadd(vba, vmult(njb, ma));
-  L.ph.wb[ba][lane] = wba + ia * vcross(r1, njb);
-  L.ph.vb[bb][lane] = vadd(vbb, vmult(jbv, mb));
-  L.ph.wb[bb][lane] = wbb + ib * vcross(r2, jbv);
-  L.ph.v[ba][lane] = vadd(va, vmult(nj, ma));
-  L.ph.w[ba][lane] = wa + ia * vcross(r1, nj);
-  L.ph.v[bb][lane] = vadd(vb, vmult(j, mb));
-  L.ph.w[bb][lane] = wb_ + ib * vcross(r2, j);
+  st_vb(L, ba, lane, vadd(vba, vmult(njb, ma)), wba + ia * vcross(r1, njb));
+  st_vb(L, bb, lane, vadd(vbb, vmult(jbv, mb)), wbb + ib * vcross(r2, jbv));
+  st_v(L, ba, lane, vadd(va, vmult(nj, ma)), wa + ia * vcross(r1, nj));
+  st_v(L, bb, lane, vadd(vb, vmult(j, mb)), wb_ + ib * vcross(r2, j));
 }
 
 __device__ __forceinline__ void lds_box(const Lds& L, int i, int lane, Box& b) {
@@ -703,11 +738,12 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
 #pragma unroll
   for (int b = 0; b < 5; ++b) {
     L.ph.p[b][lane] = v2(E.px[b], E.py[b]);
-    L.ph.v[b][lane] = v2(E.vx[b], E.vy[b]); L.ph.w[b][lane] = E.w[b];
-    L.ph.vb[b][lane] = v2(0.0f, 0.0f); L.ph.wb[b][lane] = 0.0f;
+    st_v(L, b, lane, v2(E.vx[b], E.vy[b]), E.w[b]);
+    st_vb(L, b, lane, v2(0.0f, 0.0f), 0.0f);
   }
-  L.ph.p[5][lane] = v2(0.0f, 0.0f); L.ph.v[5][lane] = v2(0.0f, 0.0f); L.ph.vb[5][lane] = v2(0.0f, 0.0f);
-  L.ph.w[5][lane] = 0.0f; L.ph.wb[5][lane] = 0.0f;
+  L.ph.p[5][lane] = v2(0.0f, 0.0f);
+  st_v(L, 5, lane, v2(0.0f, 0.0f), 0.0f);
+  st_vb(L, 5, lane, v2(0.0f, 0.0f), 0.0f);
   const V2 ballc = v2(E.px[4], E.py[4]);
   const float BR = 10.0f;
   const float ballbb[4] = {ballc.x - BR, ballc.y - BR, ballc.x + BR, ballc.y + BR};
@@ -825,7 +861,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
       nvy = (nvy / len) * P.vmax;
     }
     E.vx[b] = nvx; E.vy[b] = nvy; E.w[b] = nw;
-    L.ph.v[b][lane] = v2(nvx, nvy); L.ph.w[b][lane] = nw;
+    st_v(L, b, lane, v2(nvx, nvy), nw);
   }
 
   STAMP(4);
@@ -842,9 +878,11 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     STAMP(5);
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
-      const V2 v = L.ph.v[b][lane], vbv = L.ph.vb[b][lane];
-      E.vx[b] = v.x; E.vy[b] = v.y; E.w[b] = L.ph.w[b][lane];
-      E.vbx[b] = vbv.x; E.vby[b] = vbv.y; E.wb[b] = L.ph.wb[b][lane];
+      V2 v, vbv;
+      ld_v(L, b, lane, v, E.w[b]);
+      ld_vb(L, b, lane, vbv, E.wb[b]);
+      E.vx[b] = v.x; E.vy[b] = v.y;
+      E.vbx[b] = vbv.x; E.vby[b] = vbv.y;
     }
     // touched arbiters' cache entries at the positions reserved in merge order
     static_for<0, KREG - 1>([&](auto kc) __attribute__((always_inline)) {
