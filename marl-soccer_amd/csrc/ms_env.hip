@@ -148,12 +148,19 @@ __device__ __forceinline__ void store_rng(const DevState& S, int64_t e, Env& E) 
 // pairs) whatever body/box each lane selects, so dynamic per-lane indexing is conflict free.
 // x/y pairs are stored together so that they load into register pairs for packed math.
 enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
-#ifndef MS_EARLY_OBS
-#define MS_EARLY_OBS 0
-#endif
 #ifndef MS_LDS_VW
 #define MS_LDS_VW 1  // body velocity + angular velocity as one 16-B LDS record (0: split arrays)
 #endif
+#ifndef MS_H2_AT
+#define MS_H2_AT 1  // t-2 snapshot load: 0 with the first batch, 1 before the solver, 2 after the physics
+#endif
+#ifndef MS_RNG_EARLY
+#define MS_RNG_EARLY 1  // PCG64 state with the first batch (0: only when a respawn is possible)
+#endif
+#ifndef MS_H1_LDS
+#define MS_H1_LDS 1  // t-1 snapshot staged in LDS across the physics (0: held in registers)
+#endif
+
 #ifndef KC
 #define KC 4  // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (rare)
 #endif
@@ -176,6 +183,11 @@ struct Lds {
   // previous step's arbiter cache, entries 0..KC-1 (loaded with the state at kernel start)
   uint32_t ch[KC][MS_BLOCK];
   float4 cj[KC][MS_BLOCK];
+#if MS_H1_LDS
+  float4 h1[7][MS_BLOCK];
+#endif
+
+
 };
 
 // body velocity (v, w) and bias velocity (vb, wb) of body b in LDS
@@ -316,6 +328,28 @@ __device__ __forceinline__ void agent_frame_store(const Params& P, const Snap& s
   unit_mag<FAST>(own_x - s.px[A], 300.0f - s.py[A], f + 16);
   unit_mag<FAST>(opp_x - s.px[A], 300.0f - s.py[A], f + 19);
   float* d = row0 + A * 66 + K * 22;
+#if MS_ABLATE == 7  // timing ablation: the same bytes, lane-interleaved (coalesced 1-KiB stores)
+  {
+    const int ln = threadIdx.x & 63;
+    float* wb = row0 - ln * 264;
+    auto put = [&](int off, const float* v, int nf) {
+      // 16-B pieces to their slot start, 8-B pieces to their own position: in bounds, aligned
+      if (nf == 4) *(float4*)(wb + (off / 4) * 256 + ln * 4) = make_float4(v[0], v[1], v[2], v[3]);
+      else *(float2*)(wb + (off / 4) * 256 + ln * 4 + (off % 4)) = make_float2(v[0], v[1]);
+    };
+    const int o = A * 66 + K * 22;
+    if constexpr (((A + K) & 1) == 0) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) put(o + 4 * q, f + 4 * q, 4);
+      put(o + 20, f + 20, 2);
+    } else {
+      put(o, f, 2);
+#pragma unroll
+      for (int q = 0; q < 5; ++q) put(o + 2 + 4 * q, f + 2 + 4 * q, 4);
+    }
+    return;
+  }
+#endif
   if constexpr (((A + K) & 1) == 0) {  // 16-B aligned: five 16-B stores and one 8-B store
 #pragma unroll
     for (int q = 0; q < 5; ++q) obs_put((float4*)(d + 4 * q), make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]));
@@ -394,6 +428,31 @@ __device__ __forceinline__ void emit_three(const Params& P, const Snap& s2, cons
 
 // Frames of a reset (soccer_env.py:90-96): all three stacked frames are the current one, and
 // the history slot (t-2 for the next step) is the current snapshot too.
+#if MS_H1_LDS
+__device__ __forceinline__ void snap_to_lds(Lds& L, int lane, const Snap& s) {
+  float f[28];
+#pragma unroll
+  for (int b = 0; b < 5; ++b) { f[b] = s.px[b]; f[5 + b] = s.py[b]; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { f[10 + i] = s.vx[i]; f[14 + i] = s.vy[i]; f[18 + i] = s.ang[i]; f[22 + i] = s.w[i]; }
+  f[26] = 0.0f; f[27] = 0.0f;
+#pragma unroll
+  for (int g = 0; g < 7; ++g) L.h1[g][lane] = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
+}
+__device__ __forceinline__ void snap_from_lds(const Lds& L, int lane, Snap& s) {
+  float f[28];
+#pragma unroll
+  for (int g = 0; g < 7; ++g) {
+    const float4 v = L.h1[g][lane];
+    f[4 * g] = v.x; f[4 * g + 1] = v.y; f[4 * g + 2] = v.z; f[4 * g + 3] = v.w;
+  }
+#pragma unroll
+  for (int b = 0; b < 5; ++b) { s.px[b] = f[b]; s.py[b] = f[5 + b]; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { s.vx[i] = f[10 + i]; s.vy[i] = f[14 + i]; s.ang[i] = f[18 + i]; s.w[i] = f[22 + i]; }
+}
+#endif
+
 __device__ __forceinline__ void emit_fill3(const DevState& S, const Params& P, int64_t e, const Snap& s0,
                                            float* __restrict__ obs) {
   if (obs && MS_ABLATE != 3) {
@@ -712,7 +771,7 @@ __device__ __forceinline__ void write_arbiter_cache(const DevState& S, int npar,
 
 __device__ __forceinline__ void physics_step(const DevState& S, const Params& P, int64_t e, Env& E, float fx[4],
                                              float fy[4], float tq[4], Lds& L, int lane,
-                                             unsigned long long* overflow_acc) {
+                                             unsigned long long* overflow_acc, Snap& h2) {
   const float dt = P.dt;
   // cpBodyUpdatePosition
 #pragma unroll
@@ -865,6 +924,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
   }
 
   STAMP(4);
+  if (MS_H2_AT == 1) snap_load(S, e, h2);  // arrives during the solver
   if (C.nc > 0) {
     // cpArbiterApplyCachedImpulse, then cpArbiterApplyImpulse x 10 (pymunk Space default)
     FOR_CONTACTS(C, ovf, warm_one(P, c_, L, lane));
@@ -969,7 +1029,7 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   unpack_scalars(S.I4[el], E);
   load_bodies(S, el, E);
   Snap h2;  // obs-history snapshot t-2
-  if (MS_ABLATE != 6) snap_load(S, el, h2);
+  if (MS_ABLATE != 6 && MS_H2_AT == 0) snap_load(S, el, h2);
   float a[12];
   {
     const float4* ap = (const float4*)(actions + el * 12);
@@ -1002,10 +1062,13 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
 
   stage_segments(P, L, lane);
   bool fill3 = false, rng_loaded = false, rng_dirty = false;
+#if MS_RNG_EARLY
+  // PCG64 for goal respawns and auto-resets, with the first batch for every lane: 32 B/env
+  // more in the start burst instead of a dependent HBM round trip in most waves
+  load_rng(S, el, E);
+  rng_loaded = true;
+#endif
   Snap h1;  // obs-history snapshot t-1: the body state before this step
-  // frames t-2 and t-1 before the physics (MS_EARLY_OBS 1: every block, 2: odd blocks) or with
-  // frame t at the end (0)
-  const bool early = MS_EARLY_OBS == 1 || (MS_EARLY_OBS == 2 && (blockIdx.x & 1));
   if (active) {
     // SoccerEnv.step validation (soccer_env.py:101-117): a non-finite action skips the env
     bool finite = true;
@@ -1020,24 +1083,21 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   if (active) {
     E.steps += 1;
     const bool done_now = P.max_steps > 0 && E.steps >= P.max_steps;
+#if !MS_RNG_EARLY
     // PCG64 state now if this step may respawn (ball within 30 px of a goal mouth — it moves
     // <= 4 px per step — or the episode ends here)
     if (((E.px[4] < 40.0f || E.px[4] > 760.0f) && E.py[4] > 195.0f && E.py[4] < 405.0f) || (P.autoreset && done_now)) {
       load_rng(S, e, E);
       rng_loaded = true;
     }
-    // (2) frames t-2 and t-1; the stack is refilled instead after a reset (hist_empty) or an
-    // auto-reset at the end of this step
+#endif
+    // the stack is refilled instead of shifted after a reset (hist_empty) or an auto-reset at
+    // the end of this step
     fill3 = (E.meta & META_HE) != 0 || (P.autoreset && done_now);
     snap_of(E, h1);
-    if (!fill3 && early) {
-      if (obs && MS_ABLATE != 3) {
-        float* dst = obs + e * 264;
-        emit_snapshot<0>(P, h2, dst);
-        emit_snapshot<1>(P, h1, dst);
-      }
-      snap_store(S, e, h1);  // t-1 becomes the next step's t-2
-    }
+#if MS_H1_LDS
+    snap_to_lds(L, lane, h1);  // back at the end: not held in registers across the physics
+#endif
   }
 
   float pvx[5], pvy[5];
@@ -1060,9 +1120,16 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
       fy[i] = 0.0f + (s * F[0] + c * F[1]);
       tq[i] = F[2];
     }
+
     unsigned long long ovf = 0;
     STAMP(1);
-    physics_step(S, P, e, E, fx, fy, tq, L, lane, &ovf);
+    physics_step(S, P, e, E, fx, fy, tq, L, lane, &ovf, h2);
+    if (MS_H2_AT == 2) snap_load(S, e, h2);
+#if MS_H1_LDS
+    snap_from_lds(L, lane, h1);
+#pragma unroll
+    for (int b = 0; b < 5; ++b) { pvx[b] = h1.px[b]; pvy[b] = h1.py[b]; }
+#endif
     STAMP(7);
     if (ovf) atomicAdd(&ctr->overflow, ovf);
 
@@ -1102,8 +1169,6 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     if (fill3) {
       emit_fill3(S, P, e, s0, obs);
       E.meta &= ~META_HE;
-    } else if (early) {
-      if (obs && MS_ABLATE != 3) emit_snapshot<2>(P, s0, obs + e * 264);
     } else if (MS_ABLATE == 6) {  // frame t only, no history traffic (timing ablation)
       if (obs) emit_snapshot<2>(P, s0, obs + e * 264);
     } else {
