@@ -977,15 +977,17 @@ __device__ __forceinline__ void store_scalars(const DevState& S, int64_t e, cons
 
 // One env.step of every env (SoccerEnv.step -> Game.step, soccer_env.py:100-154,
 // game/game.py:378-437). Order inside a lane:
-//   1. every HBM read of the step is issued up front: scalars, bodies, the t-2 snapshot,
-//      actions, the old arbiter cache (entries < KC) and, when a respawn is possible, PCG64;
-//   2. frames t-2 (snapshot) and t-1 (the body state before this step IS the t-1 snapshot) of
-//      the stacked obs are emitted and the history slot is rewritten with the t-1 snapshot, so
-//      2/3 of the obs stores drain while the physics runs;
-//   3. physics, goal, rewards, outputs, resets with no further HBM reads (gfx9 has one vmcnt
-//      for loads and stores, so a read after those stores would wait for them);
-//   4. frame t and the state stores. A lane whose stack is refilled (first step after a
-//      reset, or a vec auto-reset this step) writes all three frames and the slot here.
+//   1. the first HBM batch: scalars, bodies, actions, the old arbiter cache (entries < KC,
+//      staged in LDS) and PCG64; the t-1 snapshot (= the body state before this step) is
+//      staged in LDS;
+//   2. physics; the t-2 snapshot is loaded just before the solver and arrives while it runs;
+//      no other HBM read follows (gfx9 has one vmcnt for loads and stores, so a read after
+//      the stores would wait for them);
+//   3. goal, rewards, outputs, goal respawn, vec auto-reset;
+//   4. frames t-2, t-1, t of agent 0, then agent 1, ... (each 264-B row segment in one burst
+//      of stores), the history slot (t-1 becomes the next step's t-2) and the
+//      state. A lane whose stack is refilled (first step after a reset, or an auto-reset this
+//      step) writes three copies of frame t and the slot instead.
 // The reference's default config.json physics and rewards (make_params of ms_config_default,
 // bit for bit; ms_create compares the two and launches the specialised step kernel only when
 // they are identical). As compile-time constants the masses, restitution/friction products,
