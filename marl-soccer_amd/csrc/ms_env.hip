@@ -154,6 +154,9 @@ enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
 #ifndef MS_H2_AT
 #define MS_H2_AT 1  // t-2 snapshot load: 0 with the first batch, 1 before the solver, 2 after the physics
 #endif
+#ifndef MS_P_RELOAD
+#define MS_P_RELOAD 1  // positions re-read from LDS after the physics (0: held in registers)
+#endif
 #ifndef MS_RNG_EARLY
 #define MS_RNG_EARLY 1  // PCG64 state with the first batch (0: only when a respawn is possible)
 #endif
@@ -185,6 +188,9 @@ struct Lds {
   float4 cj[KC][MS_BLOCK];
 #if MS_H1_LDS
   float4 h1[7][MS_BLOCK];
+#endif
+#if MS_H2_AT == 4
+  float4 h2[7][MS_BLOCK];
 #endif
 
 
@@ -428,8 +434,8 @@ __device__ __forceinline__ void emit_three(const Params& P, const Snap& s2, cons
 
 // Frames of a reset (soccer_env.py:90-96): all three stacked frames are the current one, and
 // the history slot (t-2 for the next step) is the current snapshot too.
-#if MS_H1_LDS
-__device__ __forceinline__ void snap_to_lds(Lds& L, int lane, const Snap& s) {
+#if MS_H1_LDS || MS_H2_AT == 4
+__device__ __forceinline__ void snap_to_lds(float4 (*dst)[MS_BLOCK], int lane, const Snap& s) {
   float f[28];
 #pragma unroll
   for (int b = 0; b < 5; ++b) { f[b] = s.px[b]; f[5 + b] = s.py[b]; }
@@ -437,13 +443,13 @@ __device__ __forceinline__ void snap_to_lds(Lds& L, int lane, const Snap& s) {
   for (int i = 0; i < 4; ++i) { f[10 + i] = s.vx[i]; f[14 + i] = s.vy[i]; f[18 + i] = s.ang[i]; f[22 + i] = s.w[i]; }
   f[26] = 0.0f; f[27] = 0.0f;
 #pragma unroll
-  for (int g = 0; g < 7; ++g) L.h1[g][lane] = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
+  for (int g = 0; g < 7; ++g) dst[g][lane] = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
 }
-__device__ __forceinline__ void snap_from_lds(const Lds& L, int lane, Snap& s) {
+__device__ __forceinline__ void snap_from_lds(const float4 (*src)[MS_BLOCK], int lane, Snap& s) {
   float f[28];
 #pragma unroll
   for (int g = 0; g < 7; ++g) {
-    const float4 v = L.h1[g][lane];
+    const float4 v = src[g][lane];
     f[4 * g] = v.x; f[4 * g + 1] = v.y; f[4 * g + 2] = v.z; f[4 * g + 3] = v.w;
   }
 #pragma unroll
@@ -1031,7 +1037,7 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   unpack_scalars(S.I4[el], E);
   load_bodies(S, el, E);
   Snap h2;  // obs-history snapshot t-2
-  if (MS_ABLATE != 6 && MS_H2_AT == 0) snap_load(S, el, h2);
+  if (MS_ABLATE != 6 && (MS_H2_AT == 0 || MS_H2_AT == 4)) snap_load(S, el, h2);
   float a[12];
   {
     const float4* ap = (const float4*)(actions + el * 12);
@@ -1097,8 +1103,11 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     // the end of this step
     fill3 = (E.meta & META_HE) != 0 || (P.autoreset && done_now);
     snap_of(E, h1);
+#if MS_H2_AT == 4
+    snap_to_lds(L.h2, lane, h2);
+#endif
 #if MS_H1_LDS
-    snap_to_lds(L, lane, h1);  // back at the end: not held in registers across the physics
+    snap_to_lds(L.h1, lane, h1);  // back at the end: not held in registers across the physics
 #endif
   }
 
@@ -1127,8 +1136,18 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     STAMP(1);
     physics_step(S, P, e, E, fx, fy, tq, L, lane, &ovf, h2);
     if (MS_H2_AT == 2) snap_load(S, e, h2);
+#if MS_H2_AT == 4
+    snap_from_lds(L.h2, lane, h2);
+#endif
+#if MS_P_RELOAD  // positions back from LDS (written by the position phase, unchanged since)
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const V2 p = L.ph.p[b][lane];
+      E.px[b] = p.x; E.py[b] = p.y;
+    }
+#endif
 #if MS_H1_LDS
-    snap_from_lds(L, lane, h1);
+    snap_from_lds(L.h1, lane, h1);
 #pragma unroll
     for (int b = 0; b < 5; ++b) { pvx[b] = h1.px[b]; pvy[b] = h1.py[b]; }
 #endif
