@@ -168,12 +168,17 @@ class SoccerBatch:
             N.check(self._L.ms_observe(self._h, self._ptr(out)), "ms_observe")
         return out
 
-    def export_state(self) -> np.ndarray:
-        """Full per-env state as a numpy ms_env_state record array (synchronises)."""
+    def export_state_raw(self) -> torch.Tensor:
+        """Full per-env state as raw ms_env_state records on the device: uint8 (N, itemsize),
+        ordered on the batch's stream (no synchronisation)."""
         buf = torch.empty((self.num_envs, N.ENV_STATE_DTYPE.itemsize), dtype=torch.uint8, device=self.device)
         with torch.cuda.device(self.device):
             N.check(self._L.ms_export_state(self._h, self._ptr(buf)), "ms_export_state")
-        host = buf.cpu().numpy()
+        return buf
+
+    def export_state(self) -> np.ndarray:
+        """Full per-env state as a numpy ms_env_state record array (synchronises)."""
+        host = self.export_state_raw().cpu().numpy()
         return host.view(N.ENV_STATE_DTYPE).reshape(self.num_envs)
 
     def import_state(self, state: np.ndarray) -> None:

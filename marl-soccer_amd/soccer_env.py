@@ -125,15 +125,35 @@ class SoccerEnv(ParallelEnv):
         return self.batch.export_state()[0]
 
     def render(self):
+        """soccer_env.py:156-162. "rgb_array" returns the (600, 800, 3) uint8 frame; "human"
+        shows it in a pygame window when pygame is installed (the reference's renderer.py
+        draws with pygame too), else raises — there is no silent no-op."""
         if self.render_mode is None:
             return None
         from marlsoccer.render import render_state
         img = render_state(self.batch.export_state()[0])
         if self.render_mode == "rgb_array":
             return img
+        try:
+            import pygame
+        except ImportError as exc:
+            raise RuntimeError("render_mode='human' needs pygame, which is not installed; use "
+                               "render_mode='rgb_array' (and marlsoccer.render.write_png)") from exc
+        if getattr(self, "_screen", None) is None:
+            pygame.init()
+            self._screen = pygame.display.set_mode((img.shape[1], img.shape[0]))
+            pygame.display.set_caption("Soccer Simulation")
+        for _ in pygame.event.get():
+            pass
+        pygame.surfarray.blit_array(self._screen, img.transpose(1, 0, 2))
+        pygame.display.flip()
         return None
 
     def close(self):
+        if getattr(self, "_screen", None) is not None:
+            import pygame
+            pygame.display.quit()
+            self._screen = None
         if self._batch is not None:
             self._batch.close()
             self._batch = None
