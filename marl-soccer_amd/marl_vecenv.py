@@ -96,13 +96,30 @@ class SyncMultiAgentVecEnv:
             e, a, _ = np.argwhere(bad)[0]
             agent = self.possible_agents[a]
             raise ValueError(f"Action contains non-finite values for agent '{agent}': {act[e, a].tolist()}")
-        out = self.batch.step(torch.from_numpy(np.ascontiguousarray(act)).to(self.batch.device))
-        obs = out.obs.cpu().numpy()
-        rew = out.rew.cpu().numpy().astype(np.float64)
-        term = out.term.cpu().numpy().astype(bool)
-        trunc = out.trunc.cpu().numpy().astype(bool)
-        infos = LazyInfos(out.score.cpu().numpy(), out.goal.cpu().numpy(), self.possible_agents)
-        return obs, rew, term, trunc, infos
+        # One round trip per step: the actions go up from a pinned staging copy and every output
+        # comes down into fresh pinned buffers (torch's caching host allocator recycles them once
+        # the caller drops the arrays), all ordered on the env's stream, then ONE synchronise.
+        # rewards are widened to float64 and the flags to bool on the device.
+        dev, st = self.batch.device, self.batch.stream
+        n = self.num_envs
+        with torch.cuda.device(dev), torch.cuda.stream(st):
+            a_h = torch.from_numpy(np.ascontiguousarray(act)).pin_memory()
+            out = self.batch.step(a_h.to(dev, non_blocking=True))
+            obs = torch.empty((n, 4, 66), dtype=torch.float32, pin_memory=True)
+            rew = torch.empty((n, 4), dtype=torch.float64, pin_memory=True)
+            term = torch.empty((n, 4), dtype=torch.bool, pin_memory=True)
+            trunc = torch.empty((n, 4), dtype=torch.bool, pin_memory=True)
+            score = torch.empty((n, 2), dtype=torch.int32, pin_memory=True)
+            goal = torch.empty((n,), dtype=torch.int8, pin_memory=True)
+            obs.copy_(out.obs, non_blocking=True)
+            rew.copy_(out.rew.to(torch.float64), non_blocking=True)
+            term.copy_(out.term.bool(), non_blocking=True)
+            trunc.copy_(out.trunc.bool(), non_blocking=True)
+            score.copy_(out.score, non_blocking=True)
+            goal.copy_(out.goal, non_blocking=True)
+            st.synchronize()
+        infos = LazyInfos(score.numpy(), goal.numpy(), self.possible_agents)
+        return obs.numpy(), rew.numpy(), term.numpy(), trunc.numpy(), infos
 
     def close(self):
         for e in self.envs:

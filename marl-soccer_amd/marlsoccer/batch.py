@@ -76,6 +76,7 @@ class SoccerBatch:
         self.trunc = torch.zeros((n, 4), dtype=torch.uint8, device=dev)
         self.goal = torch.zeros((n,), dtype=torch.int8, device=dev)
         self.score = torch.zeros((n, 2), dtype=torch.int32, device=dev)
+        self._out_ptrs = None
 
     # ---- lifecycle ---------------------------------------------------------------------
     def close(self) -> None:
@@ -127,11 +128,21 @@ class SoccerBatch:
             raise ValueError(f"actions must have shape ({self.num_envs}, 4, 3), got {tuple(actions.shape)}")
         if actions.dtype != torch.float32:
             actions = actions.float()
+        if actions.device != self.device:
+            raise ValueError(f"tensor on {actions.device}, env on {self.device}")
         actions = actions.contiguous()
-        with torch.cuda.device(self.device):
-            N.check(self._L.ms_step(self._h, self._ptr(actions), self._ptr(self.obs), self._ptr(self.rew),
-                                    self._ptr(self.term), self._ptr(self.trunc), self._ptr(self.goal),
-                                    self._ptr(self.score)), "ms_step")
+        if self._out_ptrs is None:  # the output tensors live as long as the batch
+            self._out_ptrs = tuple(self._ptr(t) for t in (self.obs, self.rew, self.term, self.trunc, self.goal,
+                                                           self.score))
+        # ms_step launches on the handle's stream; the HIP calls inside need the env's device
+        # current (switch only when it is not)
+        if torch.cuda.current_device() == self.device.index:
+            rc = self._L.ms_step(self._h, C.c_void_p(actions.data_ptr()), *self._out_ptrs)
+        else:
+            with torch.cuda.device(self.device):
+                rc = self._L.ms_step(self._h, C.c_void_p(actions.data_ptr()), *self._out_ptrs)
+        if rc:
+            N.check(rc, "ms_step")
         return StepOutput((self.obs, self.rew, self.term, self.trunc, self.goal, self.score))
 
     def step_into(self, actions: torch.Tensor, obs: torch.Tensor, rew=None, term=None, trunc=None, goal=None,
