@@ -179,6 +179,12 @@ class SoccerBatch:
             N.check(self._L.ms_observe(self._h, self._ptr(out)), "ms_observe")
         return out
 
+    @property
+    def specialised(self) -> bool:
+        """True when ms_step runs the kernel compiled for the reference's default physics and
+        rewards (ms_config_specialised)."""
+        return N.config_specialised(self._cfg)
+
     def export_state_raw(self) -> torch.Tensor:
         """Full per-env state as raw ms_env_state records on the device: uint8 (N, itemsize),
         ordered on the batch's stream (no synchronisation)."""

@@ -257,3 +257,58 @@ def test_full_size_subsample_and_invariants(ms, n, max_steps, steps):
     assert (st["body"]["py"] > -50).all() and (st["body"]["py"] < 650).all()
     assert gpu.stats()["arbiter_overflow"] == 0
     gpu.close()
+
+
+def test_corner_pileups_spill_path_bitexact(ms):
+    """All four agents and the ball wedged into the corners and pushed into them: more contacts
+    per env than the kernel's 8 register slots, so slots 9+ go through the global spill buffer
+    (SP) — the rare path of real play, held here for 80 steps — bit for bit against the oracle."""
+    n = 64
+    gpu = ms.SoccerBatch(n)  # default physics: the specialised kernel
+    assert gpu.specialised
+    gpu.reset(seed=5)
+    st = gpu.export_state()
+    rng = np.random.default_rng(0)
+    corners = [(10.0, 10.0, 1.0, 1.0), (790.0, 10.0, -1.0, 1.0), (10.0, 590.0, 1.0, -1.0), (790.0, 590.0, -1.0, -1.0)]
+    offs = [(17.0, 17.0), (47.0, 17.0), (17.0, 47.0), (47.0, 47.0)]
+    sign = np.zeros((n, 2), np.float32)
+    for i in range(n):
+        cx, cy, sx, sy = corners[i % 4]
+        sign[i] = (sx, sy)
+        for a, (ox, oy) in enumerate(offs):
+            j = rng.uniform(-1.5, 1.5, 2)
+            st["body"]["px"][i, a] = cx + sx * (ox + j[0])
+            st["body"]["py"][i, a] = cy + sy * (oy + j[1])
+            st["body"]["angle"][i, a] = rng.uniform(-0.05, 0.05)
+        st["body"]["px"][i, 4] = cx + sx * 74.0
+        st["body"]["py"][i, 4] = cy + sy * rng.uniform(13.0, 20.0)
+    for f in ("vx", "vy", "w", "vbx", "vby", "wb"):
+        st["body"][f] = 0.0
+    st["n_arb"] = 0
+    st["hist_empty"] = 1
+    gpu.import_state(st)
+    ref = orc.OracleBatch(n, "f32")
+    ref.import_state(st)
+    most = 0
+    for t in range(80):
+        act = np.zeros((n, 4, 3), np.float32)
+        act[:, :, 0] = -sign[:, None, 0]  # agents face +x (angle ~ 0): push into the corner
+        act[:, :, 1] = -sign[:, None, 1]
+        act[:, :, 2] = sh.hash_actions(n, t)[:, :, 2] * 0.2
+        out = gpu.step(torch.from_numpy(act).to(gpu.device))
+        obs, rew, trunc, goal, score, bad = ref.step(act)
+        np.testing.assert_array_equal(out.obs.cpu().numpy(), obs, err_msg=f"obs t={t}")
+        np.testing.assert_array_equal(out.rew.cpu().numpy(), rew.astype(np.float32), err_msg=f"rew t={t}")
+        g = gpu.export_state()
+        touching = (g["arb"]["idle"] == 0) & (np.arange(ms_max_arbiters())[None, :] < g["n_arb"][:, None])
+        most = max(most, int((g["arb"]["count"] * touching).sum(1).max()))
+        if t % 20 == 19:
+            assert_state_equal(g, ref.export_state(), f"t={t}")
+    assert most > 8, most  # the spill path was exercised
+    assert gpu.stats()["arbiter_overflow"] == 0 and ref.overflow() == 0
+    gpu.close()
+
+
+def ms_max_arbiters():
+    from marlsoccer import _native as N
+    return N.MAX_ARBITERS
