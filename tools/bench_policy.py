@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Policy forward variants for the device rollout (diagnostic): the reference's actor + critic
+(66-512-256-128-64-{3,1} tanh) on M = 2 x envs rows, timed with HIP events.
+
+    python tools/bench_policy.py [--envs 65536] [--iters 20]
+
+a) nn.Sequential fp32 (DeviceRollout today), b) both MLPs as one 66->1024 GEMM + batched
+(2, M, k) GEMMs per layer (fp32), c) a) under bf16 autocast, d) b) in bf16. Prints ms per
+forward and the max |difference| of the action mean and value against a).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "marl-soccer_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+    from marlsoccer.rollout import Agent
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    agent = Agent().to(dev)
+    M = 2 * a.envs
+    x = torch.randn(M, 66, device=dev).clamp(-10, 10)
+
+    def seq():
+        return agent.actor_mean(x), agent.critic(x)
+
+    lin_c = [m for m in agent.critic if isinstance(m, torch.nn.Linear)]
+    lin_a = [m for m in agent.actor_mean if isinstance(m, torch.nn.Linear)]
+
+    def pack(dtype):
+        W1 = torch.cat([lin_c[0].weight, lin_a[0].weight]).t().contiguous().to(dtype)
+        b1 = torch.cat([lin_c[0].bias, lin_a[0].bias]).to(dtype)
+        mids = [(torch.stack([lin_c[i].weight.t(), lin_a[i].weight.t()]).contiguous().to(dtype),
+                 torch.stack([lin_c[i].bias, lin_a[i].bias])[:, None, :].to(dtype)) for i in (1, 2, 3)]
+        lasts = [(lin_c[4].weight.t().contiguous().to(dtype), lin_c[4].bias.to(dtype)),
+                 (lin_a[4].weight.t().contiguous().to(dtype), lin_a[4].bias.to(dtype))]
+        return W1, b1, mids, lasts
+
+    def fused(p, dtype):
+        W1, b1, mids, lasts = p
+        h = torch.tanh(torch.addmm(b1, x.to(dtype), W1))           # (M, 1024)
+        h = h.view(M, 2, 512).transpose(0, 1)                       # (2, M, 512)
+        for W, b in mids:
+            h = torch.tanh(torch.baddbmm(b, h, W))
+        v = torch.addmm(lasts[0][1], h[0], lasts[0][0])
+        mu = torch.addmm(lasts[1][1], h[1], lasts[1][0])
+        return mu.float(), v.float()
+
+    p32, p16 = pack(torch.float32), pack(torch.bfloat16)
+    variants = {
+        "sequential_fp32": seq,
+        "fused_fp32": lambda: fused(p32, torch.float32),
+        "sequential_bf16_autocast": lambda: torch.autocast("cuda", dtype=torch.bfloat16)(seq)(),
+        "fused_bf16": lambda: fused(p16, torch.bfloat16),
+    }
+    with torch.no_grad():
+        ref_mu, ref_v = seq()
+        for name, fn in variants.items():
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                mu, v = fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            print(json.dumps({"variant": name, "rows": M, "ms_per_forward": ms,
+                              "max_abs_diff_mean": float((mu.float() - ref_mu).abs().max()),
+                              "max_abs_diff_value": float((v.float() - ref_v).abs().max())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
