@@ -27,6 +27,55 @@ def dist_env() -> tuple:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+# per-env step-output record for the whole-batch gather: obs (4, 66) f32, rew (4,) f32,
+# term (4,) u8, trunc (4,) u8, goal () i8, score (2,) i32 — 1,089 bytes, packed as raw bytes so
+# that one collective moves all of them
+_FIELDS = (("obs", (4, 66), "float32"), ("rew", (4,), "float32"), ("term", (4,), "uint8"),
+           ("trunc", (4,), "uint8"), ("goal", (), "int8"), ("score", (2,), "int32"))
+
+
+def _nbytes(shape, dtype):
+    import numpy as np
+    return int(np.prod(shape, dtype=np.int64)) * np.dtype(dtype).itemsize
+
+
+RECORD_BYTES = sum(_nbytes(sh, dt) for _, sh, dt in _FIELDS)
+
+
+def pack_step_outputs(out: dict):
+    """{obs, rew, term, trunc, goal, score} tensors of n envs -> uint8 (n, RECORD_BYTES), one
+    device copy per field."""
+    import torch
+    n = out["obs"].shape[0]
+    parts = [out[name].contiguous().view(torch.uint8).reshape(n, -1) for name, _, _ in _FIELDS]
+    return torch.cat(parts, dim=1)
+
+
+def unpack_step_outputs(buf) -> dict:
+    """Inverse of pack_step_outputs: views into buf (m, RECORD_BYTES)."""
+    import torch
+    m, off, out = buf.shape[0], 0, {}
+    for name, shape, dt in _FIELDS:
+        nb = _nbytes(shape, dt)
+        out[name] = buf[:, off:off + nb].contiguous().view(getattr(torch, dt)).reshape((m,) + tuple(shape))
+        off += nb
+    return out
+
+
+def all_gather_rows(buf, world: int, group=None):
+    """Concatenate every rank's (n, k) tensor along dim 0 (equal n): all_gather_into_tensor on
+    RCCL, the list form on backends without it (gloo, used by the CPU tests)."""
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend(group) == "nccl":
+        dst = torch.empty((world * buf.shape[0],) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device)
+        dist.all_gather_into_tensor(dst, buf, group=group)
+        return dst
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    return torch.cat(parts, dim=0)
+
+
 class ShardedSoccerEnv:
     """This rank's shard of a global batch of envs on its own GPU.
 
@@ -69,6 +118,19 @@ class ShardedSoccerEnv:
             self._gathered = torch.empty((self.global_envs, 4, 66), dtype=torch.float32, device=self.device)
         dist.all_gather_into_tensor(self._gathered, self.batch.obs, group=self.group)
         return self._gathered
+
+    def gather_outputs(self) -> dict:
+        """Every rank's last step outputs (obs, rew, term, trunc, goal, score) for the whole
+        batch, in global env order, on every rank: ONE all-gather over a packed 1,089-B-per-env
+        record instead of one collective per tensor. Requires equal shard sizes."""
+        if self.world > 1 and self.global_envs % self.world:
+            raise ValueError("gather_outputs needs global_envs divisible by the world size")
+        b = self.batch
+        buf = pack_step_outputs({"obs": b.obs, "rew": b.rew, "term": b.term, "trunc": b.trunc, "goal": b.goal,
+                                 "score": b.score})
+        if self.world > 1:
+            buf = all_gather_rows(buf, self.world, self.group)
+        return unpack_step_outputs(buf)
 
     def close(self):
         self.batch.close()

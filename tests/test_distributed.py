@@ -44,7 +44,7 @@ def _worker(rank, world, port, G, steps, q):
     sys.path[:0] = [os.path.join(root, "tests"), os.path.join(root, "oracle"), os.path.join(root, "marl-soccer_amd")]
     import oracle as orc
     import sim_helpers as sh
-    from marlsoccer.distributed import shard_range as sr
+    from marlsoccer.distributed import all_gather_rows, pack_step_outputs, shard_range as sr
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -52,13 +52,19 @@ def _worker(rank, world, port, G, steps, q):
     env = orc.OracleBatch(count, "f32", orc.default_config(max_steps=40))
     env.reset(np.stack([orc.pcg_from_seed(19 + start + i) for i in range(count)]), 0)
     for t in range(steps):
-        obs = env.step(sh.hash_actions(count, t, env0=start))[0]
+        obs, rew, trunc, goal, score, _ = env.step(sh.hash_actions(count, t, env0=start))
     parts = [torch.empty((count, 4, 66)) for _ in range(world)]
     dist.all_gather(parts, torch.from_numpy(obs))
+    # ShardedSoccerEnv.gather_outputs' packed single collective (gloo form of all_gather_rows)
+    packed = pack_step_outputs({
+        "obs": torch.from_numpy(obs), "rew": torch.from_numpy(np.asarray(rew, np.float32)),
+        "term": torch.zeros((count, 4), dtype=torch.uint8), "trunc": torch.from_numpy(np.asarray(trunc, np.uint8)),
+        "goal": torch.from_numpy(np.asarray(goal, np.int8)), "score": torch.from_numpy(np.asarray(score, np.int32))})
+    packed_all = all_gather_rows(packed, world)
     elapsed = torch.tensor([float(rank + 1)])
     dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)  # bench.py's max-over-ranks timing
     if rank == 0:
-        q.put((torch.cat(parts).numpy(), float(elapsed)))
+        q.put((torch.cat(parts).numpy(), float(elapsed), packed_all.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -74,7 +80,7 @@ def test_gloo_world2_sharded_equals_single_process():
     procs = [ctx.Process(target=_worker, args=(r, world, port, G, steps, q)) for r in range(world)]
     for p in procs:
         p.start()
-    gathered, tmax = q.get(timeout=300)
+    gathered, tmax, packed_all = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -82,5 +88,14 @@ def test_gloo_world2_sharded_equals_single_process():
     single = orc.OracleBatch(G, "f32", orc.default_config(max_steps=40))
     single.reset(np.stack([orc.pcg_from_seed(19 + i) for i in range(G)]), 0)
     for t in range(steps):
-        obs = single.step(sh.hash_actions(G, t))[0]
+        obs, rew, trunc, goal, score, _ = single.step(sh.hash_actions(G, t))
     np.testing.assert_array_equal(gathered, obs)
+    from marlsoccer.distributed import RECORD_BYTES, unpack_step_outputs
+    assert packed_all.shape == (G, RECORD_BYTES) and RECORD_BYTES == 1089
+    got = unpack_step_outputs(torch.from_numpy(packed_all))
+    np.testing.assert_array_equal(got["obs"].numpy(), obs)
+    np.testing.assert_array_equal(got["rew"].numpy(), np.asarray(rew, np.float32))
+    np.testing.assert_array_equal(got["trunc"].numpy(), np.asarray(trunc, np.uint8))
+    np.testing.assert_array_equal(got["goal"].numpy(), np.asarray(goal, np.int8))
+    np.testing.assert_array_equal(got["score"].numpy(), np.asarray(score, np.int32))
+    assert not got["term"].numpy().any()
