@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--max-steps", type=int, default=1000,
+                    help="episode length (config.json: 1000; BASELINE configs[4]: 512)")
     ap.add_argument("--action-sets", type=int, default=0,
                     help="distinct device action buffers cycled (0: one per step, capped at --action-gib)")
     ap.add_argument("--action-gib", type=float, default=8.0, help="HBM cap for the action pool")
@@ -113,7 +115,12 @@ def main():
     from marlsoccer import SoccerBatch
 
     E = args.envs
-    batch = SoccerBatch(E, device=dev.index)
+    cfg = None
+    if args.max_steps != 1000:
+        from marlsoccer.config import load_config
+        cfg = load_config()
+        cfg["simulation"]["max_steps"] = args.max_steps
+    batch = SoccerBatch(E, config=cfg, device=dev.index)
     batch.reset(seed=19 + rank * E)  # env i of rank r seeded 19 + r*E + i (global index)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
@@ -197,11 +204,13 @@ def main():
             "dtype": "f32",
             "data": f"synthetic: uniform(-1,1) fp32 actions (device Philox, {nsets} distinct (E,4,3) buffers "
                     f"for {args.warmup + args.steps} steps, read from HBM each step); env i seeded 19+i; "
-                    "default config.json physics/rewards",
+                    "default config.json physics/rewards" + (f", max_steps={args.max_steps}" if args.max_steps != 1000 else ""),
             "config": {"workload": f"{E} parallel envs per MI355X" +
-                                   (" (BASELINE.json configs[2])" if E == 65536 else
-                                    " (BASELINE.json configs[1])" if E == 4096 else ""),
-                       "envs_per_gpu": E, "global_envs": world * E, "max_steps": 1000,
+                                   (" (BASELINE.json configs[2])" if E == 65536 and args.max_steps == 1000 else
+                                    " (BASELINE.json configs[1])" if E == 4096 and args.max_steps == 1000 else
+                                    " (BASELINE.json configs[4] per-GPU shard)" if E == 32768 and args.max_steps == 512
+                                    else ""),
+                       "envs_per_gpu": E, "global_envs": world * E, "max_steps": args.max_steps,
                        "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
