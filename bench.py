@@ -10,9 +10,13 @@ GPU (default 65,536 = BASELINE.json configs[2]), weak scaling across ranks (envs
 independent; no collective in the data path). Actions are synthetic uniform(-1, 1) fp32
 from torch's device Philox generator, one fresh (E, 4, 3) buffer per step (generated
 before the timed region, read from HBM every step). The default timed
-window is one whole episode (max_steps = 1000, including the synchronised auto-reset),
-so contact-heavy and contact-free phases are both in the average. Rank 0 prints ONE JSON
-line. --allgather adds the optional RCCL all-gather of obs (configs[3]).
+window is one whole episode of the steady state: the 1,000 warm-up steps run the first
+episode (default random spawn, as SyncMultiAgentVecEnv.reset does), whose end auto-resets
+every env with the full-random spawn the vec env uses from then on (marl_vecenv.py:45-51);
+the 1,000 timed steps are the second episode including its own auto-reset, so
+contact-heavy and contact-free phases are both in the average. (The first episode is ≈10 %
+cheaper — fewer agents start against walls — and is not what a training run sees.) Rank 0
+prints ONE JSON line. --allgather adds the optional RCCL all-gather of obs (configs[3]).
 """
 from __future__ import annotations
 
@@ -40,7 +44,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--max-steps", type=int, default=1000,
                     help="episode length (config.json: 1000; BASELINE configs[4]: 512)")
@@ -175,6 +179,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
+    # cached arbiters per env (the cache bytes of the algorithmic count), sampled mid-episode:
+    # 300 more untimed steps, so the sample is not the just-reset state at an episode boundary
+    for i in range(300):
+        launch(i)
+    torch.cuda.synchronize()
     st = batch.export_state()
     mean_arb = float(st["n_arb"].mean())
     stats = batch.stats()
@@ -217,7 +226,7 @@ def main():
                          "kernel": "ms_step_kernel", "kernel_ms": kern_ms,
                          "kernel_ms_method": "HIP events around the K back-to-back launches / K",
                          "alg_bytes_per_env_step": bytes_per_step,
-                         "mean_cached_arbiters": mean_arb,  # sampled after the timed window
+                         "mean_cached_arbiters": mean_arb,  # sampled mid-episode after the timed window
                          "pmc": pmc_info},
             "arbiter_overflow": stats["arbiter_overflow"],
         }

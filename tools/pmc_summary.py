@@ -24,7 +24,7 @@ def per_kernel(path, kernel):
     return [float(r["Counter_Value"]) for r in rows], rows
 
 
-def main(tag, envs=65536, kernel="ms_step_kernel"):
+def main(tag, envs=65536, kernel="ms_step_kernel", warmup=1000, steps=1000):
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -48,6 +48,14 @@ def main(tag, envs=65536, kernel="ms_step_kernel"):
         "lds_bytes_per_block": int(rows[0]["LDS_Block_Size"]),
         "correction": "read = 2 x FETCH_SIZE (gfx950 half-count, MI355X_MICROARCH.md HBM); write = WRITE_SIZE",
     }
+    # the bench's timed window alone (its event timing covers only those launches): dispatches
+    # [warmup, warmup + steps) of the step kernel in the kernel trace
+    tr = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))) if kernel in r["Kernel_Name"]]
+    tr.sort(key=lambda r: int(r["Dispatch_Id"]))
+    win = tr[warmup:warmup + steps]
+    if win:
+        out["kernel_avg_ns_timed_window"] = statistics.mean(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win)
+        out["timed_window_dispatches"] = [warmup, warmup + len(win)]
     for name in (f"{tag}_pmc.json", "pmc_step_kernel.json"):
         with open(os.path.join(dst, name), "w") as f:
             json.dump(out, f, indent=1)
@@ -55,4 +63,4 @@ def main(tag, envs=65536, kernel="ms_step_kernel"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 65536)  # bench.py's default window
