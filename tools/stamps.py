@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--every", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=0, help="untimed steps first (1000: steady state)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     sys.path.insert(0, PKG)
@@ -70,6 +71,9 @@ def main():
     seg = {k: [] for k in ORDER[1:]}
     seg_slow = {k: [] for k in ORDER[1:]}
     spans, totals, slow_tot, maxnc = [], [], [], []
+    for t in range(a.warmup):
+        acts.uniform_(-1.0, 1.0, generator=g)
+        env.step(acts)
     for t in range(a.steps):
         acts.uniform_(-1.0, 1.0, generator=g)
         sample = t % a.every == 0 and t > 0
@@ -98,7 +102,7 @@ def main():
                 seg[ORDER[i]].append(d.mean())
                 seg_slow[ORDER[i]].append(d[slow].mean())
     mnc = np.concatenate(maxnc)
-    res = {"envs": a.envs, "steps": a.steps, "samples": len(totals),
+    res = {"envs": a.envs, "steps": a.steps, "warmup": a.warmup, "samples": len(totals),
            "wave_cycles_mean": float(np.mean(totals)), "wave_cycles_slowest5pct": float(np.mean(slow_tot)),
            "launch_span_cycles": float(np.mean(spans)),
            "max_contacts_per_wave": {str(int(v)): int((mnc == v).sum()) for v in np.unique(mnc)},
