@@ -179,6 +179,34 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
+    # With N > 1 ranks and no --allgather: a second, shorter timed loop WITH the whole-batch
+    # obs all-gather after every step (BASELINE configs[3]; SURVEY.md 8(e) asks for the rate
+    # with and without it). Reported beside `value`, which stays the no-collective rate.
+    gather_report = None
+    if world > 1 and gathered is None and not shared:
+        gbuf = torch.empty((world * E, 4, 66), dtype=torch.float32, device=dev)
+        gk = min(200, args.steps)
+        for i in range(5):
+            launch(i)
+            dist.all_gather_into_tensor(gbuf, obs)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        for i in range(gk):
+            launch(5 + i)
+            dist.all_gather_into_tensor(gbuf, obs)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        g_el = float(gt[0])
+        gather_report = {"value": world * E * gk / g_el, "unit": "env-steps/s", "steps": gk,
+                         "ms_per_step": g_el * 1e3 / gk,
+                         "collective": f"RCCL all_gather_into_tensor of obs, {E * 1056 / 1e6:.1f} MB per rank per step"}
+        del gbuf
+
     # cached arbiters per env (the cache bytes of the algorithmic count), sampled mid-episode:
     # 300 more untimed steps, so the sample is not the just-reset state at an episode boundary
     for i in range(300):
@@ -230,6 +258,8 @@ def main():
                          "pmc": pmc_info},
             "arbiter_overflow": stats["arbiter_overflow"],
         }
+        if gather_report is not None:
+            line["with_obs_allgather"] = gather_report
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args)
             cb["gpu_over_cpu"] = value / cb["value"]
