@@ -124,6 +124,18 @@ def test_short_episodes_full_random_bitexact(ms):
     assert c["dones"] >= 96 * 7 and c["goals"] > 0, c
 
 
+def test_nondefault_physics_generic_kernel_bitexact(ms):
+    """A config with other physics (speed cap, masses, damping, torque) runs the generic step
+    kernel (parameters from the kernel arguments), bit for bit against the oracle."""
+    over = dict(max_velocity=150, agent_mass=12, ball_mass=2, agent_friction=0.95, ball_friction=0.9,
+                action_torque_max=800.0, max_steps=150)
+    from marlsoccer import _native as N
+    from marlsoccer.config import to_ms_config
+    assert not N.config_specialised(to_ms_config(cfg_dict(**over), True))
+    c = run_pair(ms, 96, 400, seed=23, **over)
+    assert c["dones"] >= 96 * 2, c
+
+
 def test_fixed_spawn_no_truncation_bitexact(ms):
     run_pair(ms, 64, 600, seed=11, mode_opts={"use_fixed_positions": True}, max_steps=0)
 
