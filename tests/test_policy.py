@@ -126,3 +126,43 @@ def test_device_rollout_deterministic_matches_host_loop():
     assert torch.equal(b1.obs, b2.obs) and torch.equal(b1.rew, b2.rew)
     b1.close()
     b2.close()
+
+
+@pytest.mark.gpu
+def test_batched_eval_matches_sequential_eval_loop():
+    """marlsoccer.evaluate (eval.py's loop, episodes as parallel envs) == eval.py's own
+    sequential loop over single SoccerEnv episodes with the same seeds. The actor's last layer is
+    set to a constant so the actions do not depend on the GEMM batch size; the red agents are
+    zero (eval.py draws them from numpy's global RNG)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer.config import load_config
+    from marlsoccer.evaluate import evaluate
+    from soccer_env import soccerenv
+    torch.manual_seed(0)
+    agent = Agent().cuda()
+    with torch.no_grad():
+        agent.actor_mean[-1].weight.zero_()
+        agent.actor_mean[-1].bias.copy_(torch.tensor([0.6, -0.4, 0.2]))
+    rms = RunningMeanStd(device="cuda")
+    cfg = load_config()
+    cfg["simulation"]["max_steps"] = 80
+    res = evaluate(agent, rms, 4, seed=7, config=cfg, red="zero", frames_every=40)
+    assert res["returns"].shape == (4, 2) and res["score"].shape == (4, 2) and res["steps"] == 80
+    assert [t for t, _ in res["frames"]] == [0, 40, 79] and res["frames"][0][1].shape == (1, 600, 800, 3)
+    for i in range(4):
+        env = soccerenv(config=cfg)
+        obs, _ = env.reset(seed=7 + i)
+        ret = np.zeros(2)
+        score = None
+        while env.agents:
+            x = rms.normalize(torch.tensor(np.stack([obs["agent_0"], obs["agent_1"]])).cuda())
+            mu = agent.get_deterministic_action(x).detach().cpu().numpy()
+            acts = {"agent_0": mu[0], "agent_1": mu[1], "agent_2": np.zeros(3, np.float32),
+                    "agent_3": np.zeros(3, np.float32)}
+            obs, rew, term, trunc, infos = env.step(acts)
+            ret += [np.float32(rew["agent_0"]), np.float32(rew["agent_1"])]
+            score = infos["agent_0"]["score"]
+        env.close()
+        np.testing.assert_array_equal(res["returns"][i], ret)
+        assert (int(res["score"][i, 0]), int(res["score"][i, 1])) == (score["blue"], score["red"])
