@@ -47,6 +47,9 @@ __device__ __forceinline__ V2 vadd(V2 a, V2 b) { return a + b; }
 __device__ __forceinline__ V2 vsub(V2 a, V2 b) { return a - b; }
 __device__ __forceinline__ V2 vneg(V2 a) { return -a; }
 __device__ __forceinline__ V2 vmult(V2 a, float s) { return a * s; }
+// c + a * s, each component one fused multiply-add (v_pk_fma_f32, one rounding): the solver's
+// velocity updates. The fp32 oracle computes the same places with fmaf (soccer_oracle.c SMADD).
+__device__ __forceinline__ V2 vmadd(V2 a, float s, V2 c) { return __builtin_elementwise_fma(a, V2{s, s}, c); }
 // a.x * b.x + a.y * b.y
 __device__ __forceinline__ float vdot(V2 a, V2 b) { const V2 p = a * b; return p.x + p.y; }
 // a.x * b.y - a.y * b.x

@@ -613,9 +613,9 @@ __device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L
   V2 va, vb;
   float wa, wbv;
   ld_v(L, ba, lane, va, wa);
-  st_v(L, ba, lane, va + vmult(nj, ma), wa + ia * vcross(c.r1, nj));
+  st_v(L, ba, lane, vmadd(nj, ma, va), __builtin_fmaf(ia, vcross(c.r1, nj), wa));
   ld_v(L, bb, lane, vb, wbv);
-  st_v(L, bb, lane, vb + vmult(j, mb), wbv + ib * vcross(c.r2, j));
+  st_v(L, bb, lane, vmadd(j, mb, vb), __builtin_fmaf(ib, vcross(c.r2, j), wbv));
 }
 
 // cpArbiterApplyImpulse for one contact
@@ -630,10 +630,10 @@ __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int
   ld_vb(L, bb, lane, vbb, wbb);
   ld_v(L, ba, lane, va, wa);
   ld_v(L, bb, lane, vb, wb_);
-  const V2 vb1 = vadd(vba, vmult(vperp(r1), wba));
-  const V2 vb2 = vadd(vbb, vmult(vperp(r2), wbb));
-  const V2 vs1 = vadd(va, vmult(vperp(r1), wa));
-  const V2 vs2 = vadd(vb, vmult(vperp(r2), wb_));
+  const V2 vb1 = vmadd(vperp(r1), wba, vba);
+  const V2 vb2 = vmadd(vperp(r2), wbb, vbb);
+  const V2 vs1 = vmadd(vperp(r1), wa, va);
+  const V2 vs2 = vmadd(vperp(r2), wb_, vb);
   const V2 vr = vsub(vs2, vs1);
   const float vbn = vdot(vsub(vb2, vb1), n);
   const float vrn = vdot(vr, n);
@@ -658,10 +658,10 @@ __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int
   const V2 nj = vneg(j);
   // body a first, then body b (apply_bias_impulses then apply_impulses, cpArbiter.c);
   // a and b are distinct bodies, so the four updates commute per body.
-  st_vb(L, ba, lane, vadd(vba, vmult(njb, ma)), wba + ia * vcross(r1, njb));
-  st_vb(L, bb, lane, vadd(vbb, vmult(jbv, mb)), wbb + ib * vcross(r2, jbv));
-  st_v(L, ba, lane, vadd(va, vmult(nj, ma)), wa + ia * vcross(r1, nj));
-  st_v(L, bb, lane, vadd(vb, vmult(j, mb)), wb_ + ib * vcross(r2, j));
+  st_vb(L, ba, lane, vmadd(njb, ma, vba), __builtin_fmaf(ia, vcross(r1, njb), wba));
+  st_vb(L, bb, lane, vmadd(jbv, mb, vbb), __builtin_fmaf(ib, vcross(r2, jbv), wbb));
+  st_v(L, ba, lane, vmadd(nj, ma, va), __builtin_fmaf(ia, vcross(r1, nj), wa));
+  st_v(L, bb, lane, vmadd(j, mb, vb), __builtin_fmaf(ib, vcross(r2, j), wb_));
 }
 
 __device__ __forceinline__ void lds_box(const Lds& L, int i, int lane, Box& b) {

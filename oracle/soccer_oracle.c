@@ -516,15 +516,26 @@ static inline real k_scalar_body(real m_inv, real i_inv, vec r, vec n) {
   return m_inv + i_inv * rcn * rcn;
 }
 
+/* c + a * b in the solver (cpArbiterApplyImpulse / ApplyCachedImpulse velocity updates and
+ * relative velocities). The f32 build is the HIP kernel's contract, which fuses these into
+ * fused multiply-adds (one rounding, ms_device.h vmadd); the f64 build keeps Chipmunk's
+ * separate multiply and add (the golden fixtures were captured with it). */
+#if defined(ORC_F32)
+#define SMADD(a, b, c) fmaf((a), (b), (c))
+#else
+#define SMADD(a, b, c) ((a) * (b) + (c))
+#endif
+static inline vec vmadd(vec a, real s, vec c) { return v2(SMADD(a.x, s, c.x), SMADD(a.y, s, c.y)); }
+
 static void apply_impulse(orc_body *b, real m_inv, real i_inv, vec j, vec r) {
-  b->vx = b->vx + j.x * m_inv;
-  b->vy = b->vy + j.y * m_inv;
-  b->w += i_inv * vcross(r, j);
+  b->vx = SMADD(j.x, m_inv, b->vx);
+  b->vy = SMADD(j.y, m_inv, b->vy);
+  b->w = SMADD(i_inv, vcross(r, j), b->w);
 }
 static void apply_bias_impulse(orc_body *b, real m_inv, real i_inv, vec j, vec r) {
-  b->vbx = b->vbx + j.x * m_inv;
-  b->vby = b->vby + j.y * m_inv;
-  b->wb += i_inv * vcross(r, j);
+  b->vbx = SMADD(j.x, m_inv, b->vbx);
+  b->vby = SMADD(j.y, m_inv, b->vby);
+  b->wb = SMADD(i_inv, vcross(r, j), b->wb);
 }
 
 /* Phase 1: position integration, collision detection, arbiter update, prestep.
@@ -687,10 +698,10 @@ ORC_API void orc_space_phase2(orc_space *sp, const orc_params *P) {
         orc_contact *con = &arb->c[i];
         real nMass = con->nMass;
         vec r1 = con->r1, r2 = con->r2;
-        vec vb1 = vadd(v2(a->vbx, a->vby), vmult(vperp(r1), a->wb));
-        vec vb2 = vadd(v2(b->vbx, b->vby), vmult(vperp(r2), b->wb));
-        vec vs1 = vadd(v2(a->vx, a->vy), vmult(vperp(r1), a->w));
-        vec vs2 = vadd(v2(b->vx, b->vy), vmult(vperp(r2), b->w));
+        vec vb1 = vmadd(vperp(r1), a->wb, v2(a->vbx, a->vby));
+        vec vb2 = vmadd(vperp(r2), b->wb, v2(b->vbx, b->vby));
+        vec vs1 = vmadd(vperp(r1), a->w, v2(a->vx, a->vy));
+        vec vs2 = vmadd(vperp(r2), b->w, v2(b->vx, b->vy));
         vec vr = vsub(vs2, vs1);
         real vbn = vdot(vsub(vb2, vb1), n);
         real vrn = vdot(vr, n);
