@@ -271,6 +271,39 @@ def test_full_size_subsample_and_invariants(ms, n, max_steps, steps):
     gpu.close()
 
 
+def test_config5_whole_batch_one_gpu_subsample(ms):
+    """BASELINE config 5's whole batch on one GPU: 262,144 envs, max_steps=512, a whole episode
+    plus its auto-reset (560 steps). Actions are uniform(-1, 1) from the device Philox (as in the
+    bench); the 64-env subsample's rows are copied to the host and stepped through the fp32
+    oracle, whose obs, rewards and final state must match the GPU's bit for bit."""
+    n, max_steps, steps = 262144, 512, 560
+    gpu = ms.SoccerBatch(n, config=cfg_dict(max_steps=max_steps))
+    gpu.reset(seed=19)
+    sub = np.linspace(0, n - 1, 64).astype(np.int64)
+    sub_d = torch.from_numpy(sub).to(gpu.device)
+    ref = orc.OracleBatch(64, "f32", oracle_cfg(gpu._cfg))
+    ref.reset(np.stack([orc.pcg_from_seed(19 + int(i)) for i in sub]), 0)
+    gen = torch.Generator(device=gpu.device)
+    gen.manual_seed(1234)
+    dones = 0
+    for t in range(steps):
+        act = torch.rand((n, 4, 3), generator=gen, device=gpu.device) * 2.0 - 1.0
+        out = gpu.step(act)
+        robs, rrew, rtrunc = ref.step(act[sub_d].cpu().numpy())[:3]
+        dones += int(rtrunc[:, 0].sum())
+        if t % 20 == 19 or t == max_steps - 1:
+            np.testing.assert_array_equal(out.obs[sub_d].cpu().numpy(), robs, err_msg=f"obs t={t}")
+            np.testing.assert_array_equal(out.rew[sub_d].cpu().numpy(), rrew.astype(np.float32), err_msg=f"rew t={t}")
+    assert dones == 64  # every subsampled env crossed its episode end and auto-reset
+    g = gpu.export_state()
+    r = ref.export_state()
+    for f in ("px", "py", "vx", "vy", "angle", "w"):
+        np.testing.assert_array_equal(g["body"][f][sub], r["body"][f], err_msg=f"body.{f}")
+    np.testing.assert_array_equal(g["steps"][sub], r["steps"])
+    assert gpu.stats()["arbiter_overflow"] == 0
+    gpu.close()
+
+
 def test_corner_pileups_spill_path_bitexact(ms):
     """All four agents and the ball wedged into the corners and pushed into them: more contacts
     per env than the kernel's 8 register slots, so slots 9+ go through the global spill buffer
