@@ -55,8 +55,11 @@ __device__ __forceinline__ float vdot(V2 a, V2 b) { const V2 p = a * b; return p
 // a.x * b.y - a.y * b.x
 __device__ __forceinline__ float vcross(V2 a, V2 b) { const V2 p = a * b.yx; return p.x - p.y; }
 __device__ __forceinline__ V2 vperp(V2 a) { return v2(-a.y, a.x); }
-// (a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); x * -1 is an exact sign flip
-__device__ __forceinline__ V2 vrotate(V2 a, V2 b) { return a.x * b + (a.y * b.yx) * V2{-1.0f, 1.0f}; }
+// (a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x) with the outer add fused (solver impulses only;
+// the fp32 oracle's vrotate is the same SMADD form); x * -1 is an exact sign flip
+__device__ __forceinline__ V2 vrotate(V2 a, V2 b) {
+  return __builtin_elementwise_fma(V2{a.x, a.x}, b, (a.y * b.yx) * V2{-1.0f, 1.0f});
+}
 __device__ __forceinline__ float vlengthsq(V2 a) { return vdot(a, a); }
 __device__ __forceinline__ float fmaxr(float a, float b) { return (a > b) ? a : b; }  // cpfmax
 __device__ __forceinline__ float fminr(float a, float b) { return (a < b) ? a : b; }  // cpfmin

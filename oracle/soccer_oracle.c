@@ -72,7 +72,17 @@ static inline vec vmult(vec a, real s) { return v2(a.x * s, a.y * s); }
 static inline real vdot(vec a, vec b) { return a.x * b.x + a.y * b.y; }
 static inline real vcross(vec a, vec b) { return a.x * b.y - a.y * b.x; }
 static inline vec vperp(vec a) { return v2(-a.y, a.x); }
-static inline vec vrotate(vec a, vec b) { return v2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+/* c + a * b in the solver (cpArbiterApplyImpulse / ApplyCachedImpulse velocity updates and
+ * relative velocities, the impulse rotation). The f32 build is the HIP kernel's contract, which fuses these into
+ * fused multiply-adds (one rounding, ms_device.h vmadd); the f64 build keeps Chipmunk's
+ * separate multiply and add (the golden fixtures were captured with it). */
+#if defined(ORC_F32)
+#define SMADD(a, b, c) fmaf((a), (b), (c))
+#else
+#define SMADD(a, b, c) ((a) * (b) + (c))
+#endif
+/* used only by the solver and the warm start: the rotation's outer add is fused too */
+static inline vec vrotate(vec a, vec b) { return v2(SMADD(a.x, b.x, -(a.y * b.y)), SMADD(a.x, b.y, a.y * b.x)); }
 static inline real vlengthsq(vec a) { return vdot(a, a); }
 static inline real fmaxr(real a, real b) { return (a > b) ? a : b; }
 static inline real fminr(real a, real b) { return (a < b) ? a : b; }
@@ -516,15 +526,6 @@ static inline real k_scalar_body(real m_inv, real i_inv, vec r, vec n) {
   return m_inv + i_inv * rcn * rcn;
 }
 
-/* c + a * b in the solver (cpArbiterApplyImpulse / ApplyCachedImpulse velocity updates and
- * relative velocities). The f32 build is the HIP kernel's contract, which fuses these into
- * fused multiply-adds (one rounding, ms_device.h vmadd); the f64 build keeps Chipmunk's
- * separate multiply and add (the golden fixtures were captured with it). */
-#if defined(ORC_F32)
-#define SMADD(a, b, c) fmaf((a), (b), (c))
-#else
-#define SMADD(a, b, c) ((a) * (b) + (c))
-#endif
 static inline vec vmadd(vec a, real s, vec c) { return v2(SMADD(a.x, s, c.x), SMADD(a.y, s, c.y)); }
 
 static void apply_impulse(orc_body *b, real m_inv, real i_inv, vec j, vec r) {
