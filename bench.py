@@ -32,12 +32,18 @@ sys.path.insert(0, os.path.join(ROOT, "marl-soccer_amd"))
 METRIC = "env-steps/sec (4 agents × N envs) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
-# Algorithmic HBM bytes per env-step of ms_step_kernel (DESIGN.md "Roofline"):
-# actions, bodies, scalars (steps, score, meta, PCG64 buffered u32), the t-2 obs-history snapshot
-# (26 f32; the t-1 snapshot is the body state itself)
-ALG_READ = 48 + 176 + 16 + 104
-ALG_WRITE = 176 + 16 + 104 + 1056 + 16 + 4 + 4 + 1 + 8  # bodies, scalars, snapshot, obs, rew, term, trunc, goal, score
-ARB_BYTES = 20                       # one cached arbiter: header + 4 impulses (read + rewritten)
+# Algorithmic HBM bytes per env-step, SURVEY.md §8(d): B_step = 2,289 + 2·C, where C is the
+# warm-start (arbiter) cache read and written per env-step. reads: actions 48, bodies 180,
+# episode scalars 16, RNG 40, two prior obs frames 704; writes: bodies 180, scalars 16, RNG 24,
+# obs 1,056, rewards 16, term/trunc 8, goal 1. C from this build's layout: 20 B per cached
+# arbiter (4-B header + 4 accumulated impulses) × the mean number of cached arbiters per env.
+# roofline.achieved uses this figure (the task's definition); the bytes this layout actually
+# moves (the t-2 history as a 104-B snapshot instead of two 352-B frames, RNG
+# only on respawns) are reported beside it as layout_bytes_per_env_step.
+SURVEY_BYTES = 2289
+ARB_BYTES = 20
+LAYOUT_READ = 48 + 176 + 16 + 104
+LAYOUT_WRITE = 176 + 16 + 104 + 1056 + 16 + 4 + 4 + 1 + 8  # bodies, scalars, snapshot, obs, rew, term, trunc, goal, score
 
 
 def parse():
@@ -54,24 +60,49 @@ def parse():
     ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of obs after every step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-envs", type=int, default=65536)
-    ap.add_argument("--cpu-steps", type=int, default=3000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target wall time of the all-cores CPU baseline (its step count is sized from the "
+                         "single-core leg)")
     return ap.parse_args()
 
 
+def cgroup_cpu_limit():
+    """CPUs this process may use per the cgroup CPU quota (None when unlimited or unknown)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:  # cgroup v2: "<quota> <period>" or "max <period>"
+            q, p = f.read().split()[:2]
+            return None if q == "max" else max(1, int(int(q) // int(p)))
+    except Exception:
+        pass
+    try:  # cgroup v1
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return None if q <= 0 else max(1, q // p)
+    except Exception:
+        return None
+
+
 def cpu_baseline(args):
-    """The oracle's f64 restatement (reference precision) on this host's cores, bounded."""
+    """The oracle's f64 restatement (reference precision) on every host core this process may
+    use (the serial one-env-at-a-time loop on one core, and all cores over env
+    shards); bounded to about --cpu-seconds of wall time."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     try:
-        cores = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except Exception:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    n, k = args.cpu_envs, args.cpu_steps
-    secs = orc.cpu_baseline(n, k, cores, "f64")
-    # SURVEY.md §8(d): also the serial one-env-at-a-time loop on one core
+        affinity = os.cpu_count() or 1
+    quota = cgroup_cpu_limit()
+    cores = max(1, min(affinity, quota) if quota else affinity)
+    # SURVEY.md §8(d): the serial one-env-at-a-time loop on one core (marl_vecenv.py:39)
     n1, k1 = 4096, 500
     secs1 = orc.cpu_baseline(n1, k1, 1, "f64")
+    rate1 = n1 * k1 / secs1
+    n = args.cpu_envs
+    k = max(100, int(args.cpu_seconds * rate1 * cores / n))
+    secs = orc.cpu_baseline(n, k, cores, "f64")
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -80,9 +111,24 @@ def cpu_baseline(args):
         pass
     return {"value": n * k / secs, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "sample": f"oracle f64 (C restatement of Game.step + Chipmunk) {n} envs x {k} steps, "
-                      f"random actions, {cores} threads, {secs:.2f} s wall",
-            "single_core": {"value": n1 * k1 / secs1, "sample": f"{n1} envs x {k1} steps, 1 thread, {secs1:.2f} s"},
-            "host": {"cpu_count": os.cpu_count(), "model": model}}
+                      f"random actions, {cores} threads (every CPU this process may use), {secs:.2f} s wall",
+            "single_core": {"value": rate1, "sample": f"{n1} envs x {k1} steps, 1 thread, {secs1:.2f} s"},
+            "host": {"cpu_count": os.cpu_count(), "affinity": affinity, "cgroup_cpu_limit": quota, "model": model}}
+
+
+def regime(warmup: int, steps: int, max_steps: int) -> str:
+    """Which part of the episode cycle the timed window covers (the cost of a step depends on
+    it: DESIGN.md §7)."""
+    if max_steps <= 0:
+        return f"steps {warmup}-{warmup + steps} of one unbounded episode (default random spawn)"
+    first, last = warmup // max_steps, (warmup + steps - 1) // max_steps
+    if last == 0:
+        return (f"first episode only, steps {warmup}-{warmup + steps} of {max_steps} (default random spawn; "
+                "cheaper than the steady state: DESIGN.md §7)")
+    if first >= 1 and steps >= max_steps:
+        return f"steady state: {steps} steps from step {warmup} (episodes {first + 1}-{last + 1}, full-random respawns)"
+    return (f"steps {warmup}-{warmup + steps} (episodes {first + 1}-{last + 1}; episode 1 has the default random "
+            "spawn, later ones the full-random respawn)")
 
 
 def load_pmc_traffic():
@@ -215,18 +261,25 @@ def main():
     st = batch.export_state()
     mean_arb = float(st["n_arb"].mean())
     stats = batch.stats()
-    bytes_per_step = ALG_READ + ALG_WRITE + 2 * ARB_BYTES * mean_arb
+    bytes_per_step = SURVEY_BYTES + 2 * ARB_BYTES * mean_arb
+    layout_bytes = LAYOUT_READ + LAYOUT_WRITE + 2 * ARB_BYTES * mean_arb
     achieved = bytes_per_step * E / (kern_ms * 1e-3) / 1e9
+    window = regime(args.warmup, args.steps, args.max_steps)
+    steady = window.startswith("steady state")
     value = world * E * args.steps / elapsed
     if rank == 0:
         pmc = load_pmc_traffic()
         traffic = None
         pmc_info = None
         if pmc and pmc.get("envs") == E:
-            # HBM bytes per launch from the committed rocprofv3 PMC passes, over the live kernel time
-            traffic = pmc["hbm_bytes_per_launch"] / (kern_ms * 1e-3) / 1e9
+            # HBM bytes per launch from the committed rocprofv3 PMC passes (a steady-state
+            # window); divided by this run's kernel time only when this run timed the same regime
             pmc_info = {"source": f"profiles/{pmc['tag']}_pmc.json", "bytes_per_launch": pmc["hbm_bytes_per_launch"],
-                        "alg_bytes_per_launch": bytes_per_step * E}
+                        "regime": pmc.get("regime", "steady state (warmup 1000, 200 steps)"),
+                        "alg_bytes_per_launch": bytes_per_step * E,
+                        "layout_bytes_per_launch": layout_bytes * E}
+            if steady:
+                traffic = pmc["hbm_bytes_per_launch"] / (kern_ms * 1e-3) / 1e9
         line = {
             "metric": METRIC,
             "value": value,
@@ -254,8 +307,15 @@ def main():
                          "kernel": "ms_step_kernel", "kernel_ms": kern_ms,
                          "kernel_ms_method": "HIP events around the K back-to-back launches / K",
                          "alg_bytes_per_env_step": bytes_per_step,
+                         "alg_bytes_source": "SURVEY.md §8(d): 2,289 + 2 x 20 B x mean cached arbiters",
+                         "layout_bytes_per_env_step": layout_bytes,
+                         "traffic_source": (pmc_info["source"] + " (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch) "
+                                            "over this run's kernel_ms") if traffic is not None else
+                                           ("not this regime: the committed PMC counters are steady-state "
+                                            "(see pmc)") if pmc_info else None,
                          "mean_cached_arbiters": mean_arb,  # sampled mid-episode after the timed window
                          "pmc": pmc_info},
+            "regime": window,
             "arbiter_overflow": stats["arbiter_overflow"],
         }
         if gather_report is not None:

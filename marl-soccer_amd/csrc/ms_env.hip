@@ -1085,6 +1085,9 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     if (!finite) {
       atomicAdd(&ctr->nonfinite, 1ULL);
       atomicMin(&ctr->first_bad, (long long)e);
+      // the env is not stepped; its reward is poisoned so that no caller reads the previous
+      // step's value as this one's (the reference raises ValueError here)
+      if (rew) *(float4*)(rew + e * 4) = make_float4(__builtin_nanf(""), __builtin_nanf(""), 0.0f, 0.0f);
       active = false;
     }
   }

@@ -99,6 +99,26 @@ class SoccerBatch:
             raise ValueError("tensor must be contiguous")
         return C.c_void_p(t.data_ptr())
 
+    # ---- stream ordering ---------------------------------------------------------------
+    # Kernels run on self.stream. Inputs are produced, and outputs consumed, on the caller's
+    # current stream; when the two differ the env's stream waits for the caller's work before a
+    # launch and the caller's stream waits for the launch after it, and temporaries made for
+    # the launch are recorded on the env's stream so the caching allocator cannot hand their
+    # blocks out while the kernel still reads them.
+    def _enter(self):
+        cur = torch.cuda.current_stream(self.device)
+        if cur != self.stream:
+            self.stream.wait_stream(cur)
+            return cur
+        return None
+
+    def _leave(self, cur, *temps):
+        if cur is not None:
+            for t in temps:
+                if t is not None:
+                    t.record_stream(self.stream)
+            cur.wait_stream(self.stream)
+
     # ---- API ---------------------------------------------------------------------------
     def reset(self, seed=None, options=None, mask: torch.Tensor | None = None, out: torch.Tensor | None = None):
         """Game.reset for every env (or the envs selected by `mask`).
@@ -119,11 +139,19 @@ class SoccerBatch:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
         obs = self.obs if out is None else out
         with torch.cuda.device(self.device):
+            cur = self._enter()
             N.check(self._L.ms_reset(self._h, self._ptr(pcg_t), self._ptr(m), mode, self._ptr(obs)), "ms_reset")
+            self._leave(cur, pcg_t, m)
         return obs
 
-    def step(self, actions: torch.Tensor) -> StepOutput:
-        """One env.step for all envs; actions (N, 4, 3) float32 on the env's device."""
+    def step(self, actions: torch.Tensor, check: bool = False) -> StepOutput:
+        """One env.step for all envs; actions (N, 4, 3) float32 on the env's device.
+
+        An env whose actions are not all finite is not stepped: its reward comes back NaN and
+        the library counts it (ms_get_stats). check=True synchronises and raises the
+        reference's ValueError (soccer_env.py:116-117) for the first such env; otherwise call
+        raise_if_nonfinite() at a point that synchronises anyway (DeviceRollout does, once
+        per rollout)."""
         if actions.shape != (self.num_envs, 4, 3):
             raise ValueError(f"actions must have shape ({self.num_envs}, 4, 3), got {tuple(actions.shape)}")
         if actions.dtype != torch.float32:
@@ -137,20 +165,47 @@ class SoccerBatch:
         # ms_step launches on the handle's stream; the HIP calls inside need the env's device
         # current (switch only when it is not)
         if torch.cuda.current_device() == self.device.index:
+            cur = self._enter()
             rc = self._L.ms_step(self._h, C.c_void_p(actions.data_ptr()), *self._out_ptrs)
+            self._leave(cur, actions)
         else:
             with torch.cuda.device(self.device):
+                cur = self._enter()
                 rc = self._L.ms_step(self._h, C.c_void_p(actions.data_ptr()), *self._out_ptrs)
+                self._leave(cur, actions)
         if rc:
             N.check(rc, "ms_step")
+        if check:
+            self.raise_if_nonfinite(actions)
         return StepOutput((self.obs, self.rew, self.term, self.trunc, self.goal, self.score))
+
+    def raise_if_nonfinite(self, actions: torch.Tensor | None = None) -> None:
+        """Raise the reference's ValueError (soccer_env.py:116-117) if any env was handed a
+        non-finite action since the last check (synchronises the env's stream), then clear
+        the count. `actions`, when given, is the step's action tensor, used to name the agent
+        and its values as the reference's message does."""
+        st = self.stats()
+        if st["nonfinite_envs"] == 0:
+            return
+        self.reset_stats()
+        e = st["first_nonfinite_env"]
+        agent, vals = "agent_?", None
+        if actions is not None:
+            row = actions[e].detach().float().cpu().numpy()
+            bad = np.flatnonzero(~np.isfinite(row).all(axis=1))
+            a = int(bad[0]) if bad.size else 0
+            agent, vals = f"agent_{a}", row[a].tolist()
+        raise ValueError(f"Action contains non-finite values for agent '{agent}': {vals}"
+                         f" (env {e}; {st['nonfinite_envs']} env(s) not stepped)")
 
     def step_into(self, actions: torch.Tensor, obs: torch.Tensor, rew=None, term=None, trunc=None, goal=None,
                   score=None) -> None:
         """ms_step with caller-owned output tensors (any may be None except obs)."""
         with torch.cuda.device(self.device):
+            cur = self._enter()
             N.check(self._L.ms_step(self._h, self._ptr(actions), self._ptr(obs), self._ptr(rew), self._ptr(term),
                                     self._ptr(trunc), self._ptr(goal), self._ptr(score)), "ms_step")
+            self._leave(cur, actions)
 
     def launcher(self, actions: list, obs: torch.Tensor, rew=None, term=None, trunc=None, goal=None, score=None):
         """Pre-bound ms_step for a hot loop: returns f(i) that steps with actions[i % len]
@@ -176,7 +231,9 @@ class SoccerBatch:
         """Current frame of every agent, (N, 4, 22) (Game._get_observations)."""
         out = torch.empty((self.num_envs, 4, 22), dtype=torch.float32, device=self.device)
         with torch.cuda.device(self.device):
+            cur = self._enter()
             N.check(self._L.ms_observe(self._h, self._ptr(out)), "ms_observe")
+            self._leave(cur)
         return out
 
     @property
@@ -190,7 +247,9 @@ class SoccerBatch:
         ordered on the batch's stream (no synchronisation)."""
         buf = torch.empty((self.num_envs, N.ENV_STATE_DTYPE.itemsize), dtype=torch.uint8, device=self.device)
         with torch.cuda.device(self.device):
+            cur = self._enter()
             N.check(self._L.ms_export_state(self._h, self._ptr(buf)), "ms_export_state")
+            self._leave(cur)
         return buf
 
     def export_state(self) -> np.ndarray:
@@ -202,7 +261,9 @@ class SoccerBatch:
         st = np.ascontiguousarray(state, dtype=N.ENV_STATE_DTYPE).reshape(self.num_envs)
         buf = torch.from_numpy(st.view(np.uint8).reshape(self.num_envs, -1).copy()).to(self.device)
         with torch.cuda.device(self.device):
+            cur = self._enter()
             N.check(self._L.ms_import_state(self._h, self._ptr(buf)), "ms_import_state")
+            self._leave(cur, buf)
         self.synchronize()
 
     def debug_rewards(self, prev_pos, cur_pos, goal, terminal, score) -> torch.Tensor:
@@ -214,8 +275,10 @@ class SoccerBatch:
         s = torch.as_tensor(np.ascontiguousarray(score, np.int32)).to(d)
         out = torch.empty((self.num_envs, 2), dtype=torch.float32, device=d)
         with torch.cuda.device(self.device):
+            cur = self._enter()
             N.check(self._L.ms_debug_rewards(self._h, *(self._ptr(x) for x in (pv, cu, g, t, s, out))),
                     "ms_debug_rewards")
+            self._leave(cur, pv, cu, g, t, s)
         return out
 
     def stats(self) -> dict:

@@ -179,6 +179,9 @@ class DeviceRollout:
     def collect(self) -> dict:
         for t in range(self.T):
             self.step(t)
+        # the policy's actions are checked once per rollout (one synchronisation): a non-finite
+        # action raises the reference's ValueError (soccer_env.py:116-117)
+        self.batch.raise_if_nonfinite()
         if self.update_normalizer:  # notebook L347: after the rollout, from the raw observations
             self.normalizer.update(self.obs.reshape(-1, OBS_DIM))
         return {"obs": self.obs, "actions": self.actions, "logprobs": self.logprobs, "rewards": self.rewards,

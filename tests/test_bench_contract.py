@@ -16,7 +16,7 @@ def test_bench_prints_one_contract_line():
     if not torch.cuda.is_available():
         pytest.skip("needs a HIP device")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "30", "--warmup", "5",
-                        "--envs", "4096", "--cpu-envs", "512", "--cpu-steps", "50"],
+                        "--envs", "4096", "--cpu-envs", "512", "--cpu-seconds", "0.5"],
                        capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
@@ -38,3 +38,5 @@ def test_bench_prints_one_contract_line():
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
     assert cb["unit"] == "env-steps/s" and cb["sample"]
     assert d["arbiter_overflow"] == 0
+    assert d["regime"].startswith("first episode only")  # steps 5-35 of a 1,000-step episode
+    assert rl["traffic"] is None or d["regime"].startswith("steady state")

@@ -221,7 +221,51 @@ def test_nonfinite_actions_skip_env_and_count(ms):
     assert s["nonfinite_envs"] == 2 and s["first_nonfinite_env"] == 5
     np.testing.assert_array_equal(st[[5, 9]]["body"]["px"], before[[5, 9]]["body"]["px"])
     assert (st["steps"][[5, 9]] == 0).all() and (np.delete(st["steps"], [5, 9]) == 1).all()
+    rew = gpu.rew.cpu().numpy()
+    assert np.isnan(rew[[5, 9], :2]).all() and np.isfinite(np.delete(rew, [5, 9], axis=0)).all()
+    # the device path raises the reference's ValueError (soccer_env.py:116-117) when asked
+    with pytest.raises(ValueError, match=r"Action contains non-finite values for agent 'agent_2'"):
+        gpu.raise_if_nonfinite(act)
+    gpu.raise_if_nonfinite()  # the count was cleared
+    with pytest.raises(ValueError, match=r"non-finite values for agent 'agent_0'"):
+        gpu.step(act, check=True)
+    gpu.step(torch.zeros_like(act), check=True)
     gpu.close()
+
+
+def test_rollout_raises_on_nonfinite_policy_output(ms):
+    from marlsoccer.rollout import Agent, DeviceRollout, RunningMeanStd
+    n = 64
+    gpu = ms.SoccerBatch(n)
+    gpu.reset(seed=3)
+    agent = Agent().to(gpu.device)
+    with torch.no_grad():
+        agent.actor_mean[-1].bias.fill_(float("nan"))
+    ro = DeviceRollout(gpu, agent, RunningMeanStd(device=gpu.device), num_steps=4, deterministic=True)
+    with pytest.raises(ValueError, match="non-finite"):
+        ro.collect()
+    gpu.close()
+
+
+def test_side_stream_ordering(ms):
+    """A batch bound to its own stream, driven from torch's default stream with freshly made
+    action tensors: results equal a batch on the default stream (SoccerBatch orders the two
+    streams and keeps temporaries alive for the kernel)."""
+    n = 2048
+    side = torch.cuda.Stream()
+    a = ms.SoccerBatch(n, stream=side)
+    b = ms.SoccerBatch(n)
+    a.reset(seed=4)
+    b.reset(seed=4)
+    for t in range(40):
+        act = torch.from_numpy(sh.hash_actions(n, t)).to(b.device) * 1.0  # a temporary per step
+        oa = a.step(act).obs.clone()
+        ob = b.step(act).obs.clone()
+        del act
+        torch.cuda.current_stream().synchronize()
+        assert torch.equal(oa, ob), t
+    a.close()
+    b.close()
 
 
 def test_single_env_and_ragged_sizes(ms):
