@@ -44,6 +44,37 @@ class StepOutput(tuple):
     score = property(lambda s: s[5])
 
 
+# (name, dtype, per-env shape) of the packed step-output buffer, in order
+OUTPUT_LAYOUT = (("obs", torch.float32, (4, 66)), ("rew", torch.float32, (4,)), ("term", torch.uint8, (4,)),
+                 ("trunc", torch.uint8, (4,)), ("score", torch.int32, (2,)), ("goal", torch.int8, ()))
+
+
+def _region_bytes(n: int, dtype, shape) -> int:
+    k = n * dtype.itemsize
+    for d in shape:
+        k *= d
+    return (k + 15) // 16 * 16
+
+
+def output_bytes(n: int) -> int:
+    return sum(_region_bytes(n, dt, sh) for _, dt, sh in OUTPUT_LAYOUT)
+
+
+def output_views(buf, n: int) -> dict:
+    """Typed views of a packed output buffer (a torch uint8 tensor or a numpy uint8 array)."""
+    out, off = {}, 0
+    for name, dt, sh in OUTPUT_LAYOUT:
+        k = _region_bytes(n, dt, sh)
+        size = n * dt.itemsize * int(np.prod(sh, dtype=np.int64))
+        part = buf[off:off + size]
+        if isinstance(buf, torch.Tensor):
+            out[name] = part.view(dt).view((n,) + sh)
+        else:
+            out[name] = part.view(torch.empty((), dtype=dt).numpy().dtype).reshape((n,) + sh)
+        off += k
+    return out
+
+
 class SoccerBatch:
     """N independent 2v2 soccer envs on one HIP device.
 
@@ -70,12 +101,13 @@ class SoccerBatch:
                                       C.c_void_p(self.stream.cuda_stream), C.byref(h)), "ms_create")
         self._h = h
         n, dev = self.num_envs, self.device
-        self.obs = torch.zeros((n, 4, 66), dtype=torch.float32, device=dev)
-        self.rew = torch.zeros((n, 4), dtype=torch.float32, device=dev)
-        self.term = torch.zeros((n, 4), dtype=torch.uint8, device=dev)
-        self.trunc = torch.zeros((n, 4), dtype=torch.uint8, device=dev)
-        self.goal = torch.zeros((n,), dtype=torch.int8, device=dev)
-        self.score = torch.zeros((n, 2), dtype=torch.int32, device=dev)
+        # The step outputs are views of ONE device buffer (OUTPUT_LAYOUT), so a host copy of a
+        # whole step is one transfer (SoccerEnv.step). Every region starts 16-B aligned (the
+        # obs region is a multiple of 16 B for any n).
+        self.outputs = torch.zeros((output_bytes(n),), dtype=torch.uint8, device=dev)
+        v = output_views(self.outputs, n)
+        self.obs, self.rew, self.term, self.trunc = v["obs"], v["rew"], v["term"], v["trunc"]
+        self.score, self.goal = v["score"], v["goal"]
         self._out_ptrs = None
 
     # ---- lifecycle ---------------------------------------------------------------------

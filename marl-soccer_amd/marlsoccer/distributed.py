@@ -79,14 +79,17 @@ def all_gather_rows(buf, world: int, group=None):
 class ShardedSoccerEnv:
     """This rank's shard of a global batch of envs on its own GPU.
 
-    global_envs envs are split with shard_range; rank r owns [start, start + count).
+    global_envs envs are split with shard_range; rank r owns [start, start + count), each
+    env seeded with its GLOBAL index (marl_vecenv.py:18-28: env i gets seed + i), so the
+    union of the shards is the single-process batch bit for bit.
+
+    batch_factory(count, config, device_index, autoreset) builds the rank's batch; the default
+    is SoccerBatch on GPU local_rank (tests inject a CPU stand-in with the same interface).
     """
 
-    def __init__(self, global_envs: int, config: dict | None = None, autoreset: bool = True, group=None):
-        import torch
+    def __init__(self, global_envs: int, config: dict | None = None, autoreset: bool = True, group=None,
+                 batch_factory=None):
         import torch.distributed as dist
-
-        from .batch import SoccerBatch
 
         self.world, self.rank, self.local_rank = dist_env()
         if self.world > 1 and not dist.is_initialized():
@@ -94,9 +97,13 @@ class ShardedSoccerEnv:
         self.group = group
         self.global_envs = int(global_envs)
         self.start, self.count = shard_range(self.global_envs, self.world, self.rank)
-        self.device = torch.device("cuda", self.local_rank)
-        self.batch = SoccerBatch(self.count, config=config, device=self.local_rank, autoreset=autoreset)
-        self._gathered = None
+        if batch_factory is None:
+            from .batch import SoccerBatch
+
+            def batch_factory(count, cfg, dev, ar):
+                return SoccerBatch(count, config=cfg, device=dev, autoreset=ar)
+        self.batch = batch_factory(self.count, config, self.local_rank, autoreset)
+        self.device = self.batch.device
 
     def reset(self, seed: int | None = None, options=None):
         return self.batch.reset(seed=None if seed is None else int(seed) + self.start, options=options)
@@ -105,19 +112,14 @@ class ShardedSoccerEnv:
         return self.batch.step(actions)
 
     def gather_obs(self):
-        """All-gather of every rank's obs -> (global_envs, 4, 66) on every rank (RCCL).
-        Requires equal shard sizes (global_envs % world == 0)."""
-        import torch
-        import torch.distributed as dist
-
+        """All-gather of every rank's obs -> (global_envs, 4, 66) on every rank (RCCL
+        all_gather_into_tensor over xGMI; gloo's list form on CPU). Requires equal shard sizes
+        (global_envs % world == 0)."""
         if self.world == 1:
             return self.batch.obs
         if self.global_envs % self.world:
             raise ValueError("gather_obs needs global_envs divisible by the world size")
-        if self._gathered is None:
-            self._gathered = torch.empty((self.global_envs, 4, 66), dtype=torch.float32, device=self.device)
-        dist.all_gather_into_tensor(self._gathered, self.batch.obs, group=self.group)
-        return self._gathered
+        return all_gather_rows(self.batch.obs, self.world, self.group)
 
     def gather_outputs(self) -> dict:
         """Every rank's last step outputs (obs, rew, term, trunc, goal, score) for the whole

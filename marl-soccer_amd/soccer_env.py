@@ -47,6 +47,7 @@ class SoccerEnv(ParallelEnv):
         self._torque_max = float(physics.get("action_torque_max", 100000.0))
         self._device = device
         self._batch = None  # created on first use: constructing many envs stays cheap
+        self._host = None
 
     # -- lazily bound GPU env ---------------------------------------------------------------
     @property
@@ -102,12 +103,22 @@ class SoccerEnv(ParallelEnv):
 
         act = self._validate(actions)
         b = self.batch
-        out = b.step(torch.from_numpy(act).to(b.device))
-        obs = out.obs.cpu().numpy()[0]
-        r = float(out.rew.cpu().numpy()[0, 0])
-        done = bool(out.trunc.cpu().numpy()[0, 0])
-        goal = int(out.goal.cpu().numpy()[0])
-        sb, sr = (int(x) for x in out.score.cpu().numpy()[0])
+        if self._host is None:  # pinned staging: actions up, the packed step outputs down
+            from marlsoccer.batch import output_views
+            self._act_h = torch.empty((1, 4, 3), dtype=torch.float32, pin_memory=True)
+            self._host = torch.empty(b.outputs.shape, dtype=torch.uint8, pin_memory=True)
+            self._host_views = output_views(self._host.numpy(), 1)
+        with torch.cuda.device(b.device), torch.cuda.stream(b.stream):
+            self._act_h.numpy()[:] = act
+            b.step(self._act_h.to(b.device, non_blocking=True))
+            self._host.copy_(b.outputs, non_blocking=True)  # ONE device-to-host copy per step
+            b.stream.synchronize()
+        hv = self._host_views
+        obs = hv["obs"][0]
+        r = float(hv["rew"][0, 0])
+        done = bool(hv["trunc"][0, 0])
+        goal = int(hv["goal"][0])
+        sb, sr = (int(x) for x in hv["score"][0])
         observations = {a: obs[i].copy() for i, a in enumerate(self.possible_agents)}
         rewards = {"agent_0": r, "agent_1": r, "agent_2": 0.0, "agent_3": 0.0}
         terminations = {a: False for a in self.possible_agents}

@@ -69,6 +69,104 @@ def _worker(rank, world, port, G, steps, q):
     dist.destroy_process_group()
 
 
+class OracleShardBatch:
+    """CPU stand-in for SoccerBatch (the fp32 oracle behind SoccerBatch's interface: reset with an
+    int seed meaning env i gets seed + i, step, the output tensors), injected into the
+    product's ShardedSoccerEnv through its batch_factory."""
+
+    def __init__(self, count, config, device_index, autoreset):
+        import oracle as orc
+        self._orc = orc
+        self.num_envs = count
+        self.device = torch.device("cpu")
+        self.env = orc.OracleBatch(count, "f32", orc.default_config(max_steps=config["max_steps"]))
+        self.obs = torch.zeros((count, 4, 66))
+        self.rew = torch.zeros((count, 4))
+        self.term = torch.zeros((count, 4), dtype=torch.uint8)
+        self.trunc = torch.zeros((count, 4), dtype=torch.uint8)
+        self.goal = torch.zeros((count,), dtype=torch.int8)
+        self.score = torch.zeros((count, 2), dtype=torch.int32)
+
+    def reset(self, seed=None, options=None):
+        pcg = np.stack([self._orc.pcg_from_seed(int(seed) + i) for i in range(self.num_envs)])
+        self.obs[:] = torch.from_numpy(self.env.reset(pcg, 0))
+        return self.obs
+
+    def step(self, actions):
+        obs, rew, trunc, goal, score, bad = self.env.step(actions.numpy())
+        assert bad == 0
+        self.obs[:] = torch.from_numpy(obs)
+        self.rew[:] = torch.from_numpy(np.asarray(rew, np.float32))
+        self.trunc[:] = torch.from_numpy(np.asarray(trunc, np.uint8))
+        self.goal[:] = torch.from_numpy(np.asarray(goal, np.int8))
+        self.score[:] = torch.from_numpy(np.asarray(score, np.int32))
+        return self.obs, self.rew, self.term, self.trunc, self.goal, self.score
+
+    def close(self):
+        pass
+
+
+def _sharded_worker(rank, world, port, G, steps, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "tests"), os.path.join(root, "oracle"), os.path.join(root, "marl-soccer_amd")]
+    import sim_helpers as sh
+    from marlsoccer.distributed import ShardedSoccerEnv
+    from test_distributed import OracleShardBatch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    env = ShardedSoccerEnv(G, config={"max_steps": 40}, batch_factory=OracleShardBatch)
+    obs0 = env.gather_obs().clone()
+    env.reset(seed=19)
+    obs_reset = env.gather_obs().clone()
+    for t in range(steps):
+        env.step(torch.from_numpy(sh.hash_actions(env.count, t, env0=env.start)))
+    obs = env.gather_obs()
+    outs = env.gather_outputs()
+    if rank == 0:
+        q.put((env.start, env.count, obs_reset.numpy(), obs.numpy(), {k: v.numpy() for k, v in outs.items()},
+               obs0.shape))
+    dist.barrier()
+    env.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("G", [64, 66])
+def test_gloo_world2_sharded_soccer_env(G):
+    """The product's ShardedSoccerEnv on two gloo ranks (oracle-backed batches): reset(seed)
+    seeds each rank's envs with their global indices, gather_obs and gather_outputs return the
+    whole batch in global order, equal to one process stepping all G envs (60 steps of 40-step
+    episodes: every env crosses its auto-reset)."""
+    import oracle as orc
+    import sim_helpers as sh
+
+    steps, world = 60, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, G, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    start, count, obs_reset, obs, outs, shape0 = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert start == 0 and count == G // 2 and shape0 == (G, 4, 66)
+    single = orc.OracleBatch(G, "f32", orc.default_config(max_steps=40))
+    ro = single.reset(np.stack([orc.pcg_from_seed(19 + i) for i in range(G)]), 0)
+    np.testing.assert_array_equal(obs_reset, ro)
+    for t in range(steps):
+        o, rew, trunc, goal, score, _ = single.step(sh.hash_actions(G, t))
+    np.testing.assert_array_equal(obs, o)
+    np.testing.assert_array_equal(outs["obs"], o)
+    np.testing.assert_array_equal(outs["rew"], np.asarray(rew, np.float32))
+    np.testing.assert_array_equal(outs["trunc"], np.asarray(trunc, np.uint8))
+    np.testing.assert_array_equal(outs["goal"], goal)
+    np.testing.assert_array_equal(outs["score"], score)
+
+
 def test_gloo_world2_sharded_equals_single_process():
     import oracle as orc
     import sim_helpers as sh
