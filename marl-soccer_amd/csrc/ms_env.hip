@@ -6,16 +6,20 @@
 // One lane owns one env for the whole step: the physics of one env is a short sequential
 // Gauss-Seidel solve over at most a few contacts, so parallelism comes from the batch.
 //
-// HBM layout: struct of 16-byte groups. Every group array is N contiguous 16-B elements, so
-// one wave-instruction moves 1 KiB of contiguous memory and fetches four fields per lane:
-//   B4 float4 [11][N]     bodies, flat field i in group i/4 (agent b: 9b + px py vx vy angle w
-//                         vbx vby wb; ball: 36 + px py vx vy w vbx vby wb)
-//   H4 float4 [7][N]      obs-history snapshot of step t-2 (26 floats, 2 pad). The snapshot of
-//                         t-1 is the body state itself at the start of the step.
-//   I4 int4   [N]         steps, score (blue | red << 16), meta bits, PCG64 buffered u32
-//   R2 u64x2  [2][N]      PCG64 (state hi, lo), (inc hi, lo): touched by resets and goal respawns
-//   CH u32    [2][MAXA][N] arbiter-cache headers, ping-pong by a per-env parity bit
-//   CJ float4 [2][MAXA][N] arbiter-cache accumulated impulses (jn0, jt0, jn1, jt1)
+// HBM layout: state blocks. Block b holds the state of envs [64b, 64b + 64) — one wave's envs —
+// as planes of 64 lane elements (16-B elements, 4-B for the cache headers), so one wave
+// instruction moves 1 KiB of contiguous memory and fetches four fields per lane, and every plane
+// sits at a compile-time offset from the block base (no per-plane base address is held in a
+// register):
+//   B4 float4 [11][64]     bodies, flat field i in plane i/4 (agent b: 9b + px py vx vy angle w
+//                          vbx vby wb; ball: 36 + px py vx vy w vbx vby wb)
+//   H4 float4 [7][64]      obs-history snapshot of step t-2 (26 floats, 2 pad). The snapshot of
+//                          t-1 is the body state itself at the start of the step.
+//   I4 int4   [64]         steps, score (blue | red << 16), meta bits, PCG64 buffered u32
+//   R2 u64x2  [2][64]      PCG64 (state hi, lo), (inc hi, lo): touched by resets and goal respawns
+//   CH u32    [2][MAXA][64] arbiter-cache headers, ping-pong by a per-env parity bit
+//   CJ float4 [2][MAXA][64] arbiter-cache accumulated impulses (jn0, jt0, jn1, jt1)
+// The last block is padded to 64 envs; the padding lanes run with zeroed state and store nothing.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -36,9 +40,6 @@ using namespace ms;
 #ifndef MS_BLOCK
 #define MS_BLOCK 64
 #endif
-#ifndef MS_ABLATE
-#define MS_ABLATE 0  // diagnostic builds only: 1 no solver, 2 no narrowphase, 3 no obs stores, 4 no arbiter cache, 5 no history loads
-#endif
 #define MAXA MS_MAX_ARBITERS
 
 // ---- group indices -----------------------------------------------------------------------
@@ -54,17 +55,41 @@ enum {
 #define META_NC(m) (((m) >> 8) & 63)
 #define META_H32 (1u << 16)
 
+// state block layout (bytes from the block base)
+constexpr int BLK = 64;  // envs per state block = lanes per wave
+static_assert(MS_BLOCK == BLK, "the step kernel maps one wave to one state block");
+constexpr int OFF_B4 = 0;
+constexpr int OFF_H4 = OFF_B4 + G_BODY * BLK * 16;
+constexpr int OFF_I4 = OFF_H4 + G_SNAP * BLK * 16;
+constexpr int OFF_R2 = OFF_I4 + BLK * 16;
+constexpr int OFF_CH = OFF_R2 + 2 * BLK * 16;
+constexpr int OFF_CJ = OFF_CH + 2 * MAXA * BLK * 4;
+constexpr int BLOCK_BYTES = OFF_CJ + 2 * MAXA * BLK * 16;
+
 struct DevState {
   unsigned long long* stamps;  // MS_STAMPS diagnostic builds only: [wave][16] s_memtime
-  float4* B4;
-  float4* H4;
-  int4* I4;
-  ulonglong2* R2;
-  uint32_t* CH;
-  float4* CJ;
+  char* blocks;                // [ceil(n / 64)] state blocks
   void* SP;  // contact slots KREG.. of each env (pile-ups only): [env][MAXC - KREG] CSlot
   int64_t n;
 };
+
+// An env's place in the state: its block's base and its lane in the block. The step kernel
+// builds it from blockIdx.x (a wave-uniform block base); the other kernels from the env index.
+struct At {
+  char* blk;
+  int lane;
+};
+__device__ __forceinline__ At env_at(const DevState& S, int64_t e) {
+  return At{S.blocks + (int64_t)((uint64_t)e / BLK) * BLOCK_BYTES, (int)((uint64_t)e % BLK)};
+}
+// element `lane` of plane p of the region at byte offset `off` (planes of BLK elements of T)
+template <typename T>
+__device__ __forceinline__ T* plane(At a, int off, int p) {
+  return (T*)(a.blk + off + p * (BLK * (int)sizeof(T))) + a.lane;
+}
+// global-memory pointer type for the rare HBM reads that sit next to an LDS read of the same
+// value: distinct address spaces keep the compiler from merging the two into one flat load
+typedef __attribute__((address_space(1))) const uint32_t gu32_t;
 
 struct Counters {
   unsigned long long overflow;
@@ -104,17 +129,17 @@ __device__ __forceinline__ void unpack_bodies(const float f[44], Env& E) {
   E.w[4] = f[F_BALL + 4]; E.vbx[4] = f[F_BALL + 5]; E.vby[4] = f[F_BALL + 6]; E.wb[4] = f[F_BALL + 7];
 }
 
-__device__ __forceinline__ void load_bodies(const DevState& S, int64_t e, Env& E) {
+__device__ __forceinline__ void load_bodies(At a, Env& E) {
   float f[44];
 #pragma unroll
   for (int g = 0; g < G_BODY; ++g) {
-    const float4 v = S.B4[(int64_t)g * S.n + e];
+    const float4 v = *plane<float4>(a, OFF_B4, g);
     f[4 * g] = v.x; f[4 * g + 1] = v.y; f[4 * g + 2] = v.z; f[4 * g + 3] = v.w;
   }
   unpack_bodies(f, E);
 }
 
-__device__ __forceinline__ void store_bodies(const DevState& S, int64_t e, const Env& E) {
+__device__ __forceinline__ void store_bodies(At a, const Env& E) {
   float f[44];
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
@@ -125,21 +150,21 @@ __device__ __forceinline__ void store_bodies(const DevState& S, int64_t e, const
   f[F_BALL + 0] = E.px[4]; f[F_BALL + 1] = E.py[4]; f[F_BALL + 2] = E.vx[4]; f[F_BALL + 3] = E.vy[4];
   f[F_BALL + 4] = E.w[4]; f[F_BALL + 5] = E.vbx[4]; f[F_BALL + 6] = E.vby[4]; f[F_BALL + 7] = E.wb[4];
 #pragma unroll
-  for (int g = 0; g < G_BODY; ++g) S.B4[(int64_t)g * S.n + e] = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
+  for (int g = 0; g < G_BODY; ++g) *plane<float4>(a, OFF_B4, g) = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
 }
 
-__device__ __forceinline__ void load_rng(const DevState& S, int64_t e, Env& E) {
-  const ulonglong2 st = S.R2[e], inc = S.R2[S.n + e];
+__device__ __forceinline__ void load_rng(At a, Env& E) {
+  const ulonglong2 st = *plane<ulonglong2>(a, OFF_R2, 0), inc = *plane<ulonglong2>(a, OFF_R2, 1);
   E.rng.shi = st.x; E.rng.slo = st.y;
   E.rng.ihi = inc.x; E.rng.ilo = inc.y;
   E.rng.has32 = (E.meta & META_H32) ? 1u : 0u;
 }
-__device__ __forceinline__ void store_rng(const DevState& S, int64_t e, Env& E) {
+__device__ __forceinline__ void store_rng(At a, Env& E) {
   ulonglong2 st, inc;
   st.x = E.rng.shi; st.y = E.rng.slo;
   inc.x = E.rng.ihi; inc.y = E.rng.ilo;
-  S.R2[e] = st;
-  S.R2[S.n + e] = inc;
+  *plane<ulonglong2>(a, OFF_R2, 0) = st;
+  *plane<ulonglong2>(a, OFF_R2, 1) = inc;
   E.meta = (E.meta & ~META_H32) | (E.rng.has32 ? META_H32 : 0u);
 }
 
@@ -148,56 +173,27 @@ __device__ __forceinline__ void store_rng(const DevState& S, int64_t e, Env& E) 
 // pairs) whatever body/box each lane selects, so dynamic per-lane indexing is conflict free.
 // x/y pairs are stored together so that they load into register pairs for packed math.
 enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
-#ifndef MS_LDS_VW
-#define MS_LDS_VW 1  // body velocity + angular velocity as one 16-B LDS record (0: split arrays)
-#endif
-#ifndef MS_H2_AT
-#define MS_H2_AT 1  // t-2 snapshot load: 0 with the first batch, 1 before the solver, 2 after the physics
-#endif
-#ifndef MS_P_RELOAD
-#define MS_P_RELOAD 1  // positions re-read from LDS after the physics (0: held in registers)
-#endif
-#ifndef MS_RNG_EARLY
-#define MS_RNG_EARLY 1  // PCG64 state with the first batch (0: only when a respawn is possible)
-#endif
-#ifndef MS_H1_LDS
-#define MS_H1_LDS 1  // t-1 snapshot staged in LDS across the physics (0: held in registers)
+#ifndef MS_EARLY_OBS
+#define MS_EARLY_OBS 0  // 1: frames t-2, t-1 and the history slot stored before the physics
 #endif
 
-#ifndef KC
-#define KC 4  // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (rare)
-#endif
+constexpr int KC = 4;  // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (rare)
 
 struct Lds {
   Seg seg[8];  // static segments (walls, goal lines), read with per-lane indices
   struct {
     V2 p[6][MS_BLOCK];             // body position (body 5 = static, all 0)
-#if MS_LDS_VW
     float4 vw[6][MS_BLOCK];        // velocity x, y, angular velocity (one 12-B access per body)
     float4 bw[6][MS_BLOCK];        // bias velocity x, y, bias angular velocity
-#else
-    V2 v[6][MS_BLOCK];             // velocity
-    V2 vb[6][MS_BLOCK];            // bias velocity
-    float w[6][MS_BLOCK];          // angular velocity
-    float wb[6][MS_BLOCK];         // bias angular velocity
-#endif
     float box[BX_N][4][MS_BLOCK];  // agent box transform (p, cos, sin)
   } ph;
   // previous step's arbiter cache, entries 0..KC-1 (loaded with the state at kernel start)
   uint32_t ch[KC][MS_BLOCK];
   float4 cj[KC][MS_BLOCK];
-#if MS_H1_LDS
-  float4 h1[7][MS_BLOCK];
-#endif
-#if MS_H2_AT == 4
-  float4 h2[7][MS_BLOCK];
-#endif
-
-
+  float4 h1[7][MS_BLOCK];  // the t-1 snapshot (step-start state) across the physics
 };
 
 // body velocity (v, w) and bias velocity (vb, wb) of body b in LDS
-#if MS_LDS_VW
 __device__ __forceinline__ void ld_v(const Lds& L, int b, int lane, V2& v, float& w) {
   const float4 q = L.ph.vw[b][lane];
   v = v2(q.x, q.y); w = q.z;
@@ -214,12 +210,6 @@ __device__ __forceinline__ void st_vb(Lds& L, int b, int lane, V2 v, float w) {
   float* d = (float*)&L.ph.bw[b][lane];
   d[0] = v.x; d[1] = v.y; d[2] = w;
 }
-#else
-__device__ __forceinline__ void ld_v(const Lds& L, int b, int lane, V2& v, float& w) { v = L.ph.v[b][lane]; w = L.ph.w[b][lane]; }
-__device__ __forceinline__ void st_v(Lds& L, int b, int lane, V2 v, float w) { L.ph.v[b][lane] = v; L.ph.w[b][lane] = w; }
-__device__ __forceinline__ void ld_vb(const Lds& L, int b, int lane, V2& v, float& w) { v = L.ph.vb[b][lane]; w = L.ph.wb[b][lane]; }
-__device__ __forceinline__ void st_vb(Lds& L, int b, int lane, V2 v, float w) { L.ph.vb[b][lane] = v; L.ph.wb[b][lane] = w; }
-#endif
 
 // Compile-time loop: every reg[] access below uses a constant index from the first IR on,
 // so the slots are promoted to registers (an unrolled runtime loop is not: SROA runs first).
@@ -252,11 +242,11 @@ __device__ __forceinline__ void snap_of(const Env& E, Snap& s) {
   for (int i = 0; i < 4; ++i) { s.vx[i] = E.vx[i]; s.vy[i] = E.vy[i]; s.ang[i] = E.ang[i]; s.w[i] = E.w[i]; }
 }
 // the t-2 snapshot (H4): px[5] py[5] vx[4] vy[4] angle[4] w[4] in 7 float4 groups
-__device__ __forceinline__ void snap_load(const DevState& S, int64_t e, Snap& s) {
+__device__ __forceinline__ void snap_load(At a, Snap& s) {
   float f[28];
 #pragma unroll
   for (int g = 0; g < G_SNAP; ++g) {
-    const float4 v = S.H4[(int64_t)g * S.n + e];
+    const float4 v = *plane<float4>(a, OFF_H4, g);
     f[4 * g] = v.x; f[4 * g + 1] = v.y; f[4 * g + 2] = v.z; f[4 * g + 3] = v.w;
   }
 #pragma unroll
@@ -264,7 +254,7 @@ __device__ __forceinline__ void snap_load(const DevState& S, int64_t e, Snap& s)
 #pragma unroll
   for (int i = 0; i < 4; ++i) { s.vx[i] = f[10 + i]; s.vy[i] = f[14 + i]; s.ang[i] = f[18 + i]; s.w[i] = f[22 + i]; }
 }
-__device__ __forceinline__ void snap_store(const DevState& S, int64_t e, const Snap& s) {
+__device__ __forceinline__ void snap_store(At a, const Snap& s) {
   float f[28];
 #pragma unroll
   for (int b = 0; b < 5; ++b) { f[b] = s.px[b]; f[5 + b] = s.py[b]; }
@@ -272,20 +262,10 @@ __device__ __forceinline__ void snap_store(const DevState& S, int64_t e, const S
   for (int i = 0; i < 4; ++i) { f[10 + i] = s.vx[i]; f[14 + i] = s.vy[i]; f[18 + i] = s.ang[i]; f[22 + i] = s.w[i]; }
   f[26] = 0.0f; f[27] = 0.0f;
 #pragma unroll
-  for (int g = 0; g < G_SNAP; ++g) S.H4[(int64_t)g * S.n + e] = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
+  for (int g = 0; g < G_SNAP; ++g) *plane<float4>(a, OFF_H4, g) = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
 }
-#ifndef MS_NT_OBS
-#define MS_NT_OBS 0  // 1: obs stores non-temporal (variant switch)
-#endif
-typedef float F4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void obs_put(float4* d, float4 v) {
-  if constexpr (MS_NT_OBS) __builtin_nontemporal_store(F4v{v.x, v.y, v.z, v.w}, (F4v*)d);
-  else *d = v;
-}
-__device__ __forceinline__ void obs_put(float2* d, float2 v) {
-  if constexpr (MS_NT_OBS) __builtin_nontemporal_store(V2{v.x, v.y}, (V2*)d);
-  else *d = v;
-}
+__device__ __forceinline__ void obs_put(float4* d, float4 v) { *d = v; }
+__device__ __forceinline__ void obs_put(float2* d, float2 v) { *d = v; }
 
 // The six agent-agent vectors of a snapshot, computed once per pair: agent j's vector to agent
 // i is the exact negation of i's to j (IEEE a-b = -(b-a), same magnitude).
@@ -334,28 +314,6 @@ __device__ __forceinline__ void agent_frame_store(const Params& P, const Snap& s
   unit_mag<FAST>(own_x - s.px[A], 300.0f - s.py[A], f + 16);
   unit_mag<FAST>(opp_x - s.px[A], 300.0f - s.py[A], f + 19);
   float* d = row0 + A * 66 + K * 22;
-#if MS_ABLATE == 7  // timing ablation: the same bytes, lane-interleaved (coalesced 1-KiB stores)
-  {
-    const int ln = threadIdx.x & 63;
-    float* wb = row0 - ln * 264;
-    auto put = [&](int off, const float* v, int nf) {
-      // 16-B pieces to their slot start, 8-B pieces to their own position: in bounds, aligned
-      if (nf == 4) *(float4*)(wb + (off / 4) * 256 + ln * 4) = make_float4(v[0], v[1], v[2], v[3]);
-      else *(float2*)(wb + (off / 4) * 256 + ln * 4 + (off % 4)) = make_float2(v[0], v[1]);
-    };
-    const int o = A * 66 + K * 22;
-    if constexpr (((A + K) & 1) == 0) {
-#pragma unroll
-      for (int q = 0; q < 5; ++q) put(o + 4 * q, f + 4 * q, 4);
-      put(o + 20, f + 20, 2);
-    } else {
-      put(o, f, 2);
-#pragma unroll
-      for (int q = 0; q < 5; ++q) put(o + 2 + 4 * q, f + 2 + 4 * q, 4);
-    }
-    return;
-  }
-#endif
   if constexpr (((A + K) & 1) == 0) {  // 16-B aligned: five 16-B stores and one 8-B store
 #pragma unroll
     for (int q = 0; q < 5; ++q) obs_put((float4*)(d + 4 * q), make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]));
@@ -406,14 +364,11 @@ __device__ __forceinline__ void emit_snapshot(const Params& P, const Snap& s, fl
   else emit_snapshot_impl<false, K>(P, s, row0);
 }
 
-#ifndef MS_OBS_AGENT_MAJOR
-#define MS_OBS_AGENT_MAJOR 1  // 0: frame-major order (t-2 of all agents, then t-1, then t)
-#endif
 // Frames t-2, t-1, t of every agent. Agent-major order finishes each 264-B row segment of an
 // agent in one burst of stores.
 __device__ __forceinline__ void emit_three(const Params& P, const Snap& s2, const Snap& s1, const Snap& s0,
                                            float* __restrict__ row0) {
-  if (MS_OBS_AGENT_MAJOR && frame_inputs_in_range(P, s2) && frame_inputs_in_range(P, s1) &&
+  if (frame_inputs_in_range(P, s2) && frame_inputs_in_range(P, s1) &&
       frame_inputs_in_range(P, s0)) {
     float a2[6][3], a1[6][3], a0[6][3];
     pair_vectors<true>(s2, a2);
@@ -432,9 +387,25 @@ __device__ __forceinline__ void emit_three(const Params& P, const Snap& s2, cons
   }
 }
 
+// Frames t-2 and t-1 of every agent (MS_EARLY_OBS: stored before the physics).
+__device__ __forceinline__ void emit_two(const Params& P, const Snap& s2, const Snap& s1, float* __restrict__ row0) {
+  if (frame_inputs_in_range(P, s2) && frame_inputs_in_range(P, s1)) {
+    float a2[6][3], a1[6][3];
+    pair_vectors<true>(s2, a2);
+    pair_vectors<true>(s1, a1);
+    static_for<0, 4>([&](auto ac) __attribute__((always_inline)) {
+      constexpr int A = decltype(ac)::value;
+      agent_frame_store<true, A, 0>(P, s2, a2, row0);
+      agent_frame_store<true, A, 1>(P, s1, a1, row0);
+    });
+  } else {
+    emit_snapshot<0>(P, s2, row0);
+    emit_snapshot<1>(P, s1, row0);
+  }
+}
+
 // Frames of a reset (soccer_env.py:90-96): all three stacked frames are the current one, and
 // the history slot (t-2 for the next step) is the current snapshot too.
-#if MS_H1_LDS || MS_H2_AT == 4
 __device__ __forceinline__ void snap_to_lds(float4 (*dst)[MS_BLOCK], int lane, const Snap& s) {
   float f[28];
 #pragma unroll
@@ -457,17 +428,16 @@ __device__ __forceinline__ void snap_from_lds(const float4 (*src)[MS_BLOCK], int
 #pragma unroll
   for (int i = 0; i < 4; ++i) { s.vx[i] = f[10 + i]; s.vy[i] = f[14 + i]; s.ang[i] = f[18 + i]; s.w[i] = f[22 + i]; }
 }
-#endif
 
-__device__ __forceinline__ void emit_fill3(const DevState& S, const Params& P, int64_t e, const Snap& s0,
+__device__ __forceinline__ void emit_fill3(At a, const Params& P, int64_t e, const Snap& s0,
                                            float* __restrict__ obs) {
-  if (obs && MS_ABLATE != 3) {
+  if (obs) {
     float* dst = obs + e * 264;
     emit_snapshot<0>(P, s0, dst);
     emit_snapshot<1>(P, s0, dst);
     emit_snapshot<2>(P, s0, dst);
   }
-  snap_store(S, e, s0);
+  snap_store(a, s0);
 }
 
 // Game.reset (game.py:76-118): fresh bodies, score/steps 0, arbiters dropped, spawn.
@@ -534,9 +504,9 @@ struct CSlot {
 #endif
 #define MAXC (2 * MAXA)                 // contact capacity (2 per arbiter)
 
-__device__ __forceinline__ void cache_write(const DevState& S, int par, int k, int64_t e, uint32_t hdr, float4 j) {
-  S.CH[(int64_t)(par * MAXA + k) * S.n + e] = hdr;
-  S.CJ[(int64_t)(par * MAXA + k) * S.n + e] = j;
+__device__ __forceinline__ void cache_write(At a, int par, int k, uint32_t hdr, float4 j) {
+  *plane<uint32_t>(a, OFF_CH, par * MAXA + k) = hdr;
+  *plane<float4>(a, OFF_CJ, par * MAXA + k) = j;
 }
 
 // Per-lane working set of the contact pipeline.
@@ -676,52 +646,51 @@ struct CacheWalk {
   uint32_t curh;
 };
 
-// (the HBM fallback is an explicit global load: a plain select between the LDS and the global
-// element lets the optimizer form one flat-address load)
-__device__ __forceinline__ uint32_t old_hdr(const DevState& S, const Lds& L, int lane, int64_t e, int par, int k) {
-  if (k < KC) return L.ch[k][lane];
-  return __builtin_nontemporal_load(&S.CH[(int64_t)(par * MAXA + k) * S.n + e]);
+// (the HBM fallback reads through address-space-1 pointers: with generic pointers the optimizer
+// merges the LDS and the global read into one flat-address load through a selected address)
+__device__ __forceinline__ uint32_t old_hdr(At a, const Lds& L, int par, int k) {
+  if (k < KC) return L.ch[k][a.lane];
+  return __builtin_nontemporal_load((gu32_t*)plane<uint32_t>(a, OFF_CH, par * MAXA + k));
 }
-__device__ __forceinline__ float4 old_imp(const DevState& S, const Lds& L, int lane, int64_t e, int par, int k) {
-  if (k < KC) return L.cj[k][lane];
-  const float* g = (const float*)&S.CJ[(int64_t)(par * MAXA + k) * S.n + e];
-  return make_float4(__builtin_nontemporal_load(g), __builtin_nontemporal_load(g + 1), __builtin_nontemporal_load(g + 2),
-                     __builtin_nontemporal_load(g + 3));
+__device__ __forceinline__ float4 old_imp(At a, const Lds& L, int par, int k) {
+  if (k < KC) return L.cj[k][a.lane];
+  gu32_t* g = (gu32_t*)plane<float4>(a, OFF_CJ, par * MAXA + k);
+  return make_float4(__uint_as_float(__builtin_nontemporal_load(g)), __uint_as_float(__builtin_nontemporal_load(g + 1)),
+                     __uint_as_float(__builtin_nontemporal_load(g + 2)), __uint_as_float(__builtin_nontemporal_load(g + 3)));
 }
 
-__device__ __forceinline__ void cache_advance(const DevState& S, const Lds& L, int lane, int64_t e, CacheWalk& W) {
+__device__ __forceinline__ void cache_advance(At a, const Lds& L, CacheWalk& W) {
   ++W.cur;
-  W.curh = W.cur < W.nc_old ? old_hdr(S, L, lane, e, W.par, W.cur) : 0xffffffffu;
+  W.curh = W.cur < W.nc_old ? old_hdr(a, L, W.par, W.cur) : 0xffffffffu;
 }
 
 // emit the old entry under the cursor aged by one step (dropped at idle 3, cpSpaceArbiterSetFilter)
-__device__ __forceinline__ void cache_age_current(const DevState& S, const Lds& L, int lane, int64_t e, CacheWalk& W,
-                                                  unsigned long long* overflow_acc) {
+__device__ __forceinline__ void cache_age_current(At a, const Lds& L, CacheWalk& W, unsigned long long* overflow_acc) {
   const uint32_t idle = ((W.curh >> 8) & 3u) + 1u;
   if (idle < 3u) {
     if (W.out < MAXA) {
-      cache_write(S, W.par ^ 1, W.out, e, (W.curh & ~(3u << 8)) | (idle << 8), old_imp(S, L, lane, e, W.par, W.cur));
+      cache_write(a, W.par ^ 1, W.out, (W.curh & ~(3u << 8)) | (idle << 8), old_imp(a, L, W.par, W.cur));
       ++W.out;
     } else {
       (*overflow_acc)++;
     }
   }
-  cache_advance(S, L, lane, e, W);
+  cache_advance(a, L, W);
 }
 
 // cpSpaceCollideShapes + cpArbiterUpdate for one touching pair
-__device__ __forceinline__ void add_arbiter(const DevState& S, int64_t e, const Lds& L, int lane, Contacts& C,
-                                            CSlot* ovf, CacheWalk& W, int p, int ba, int bb, const Col& col, float u,
-                                            unsigned long long* overflow_acc) {
+__device__ __forceinline__ void add_arbiter(At a, const Lds& L, Contacts& C, CSlot* ovf, CacheWalk& W, int p, int ba,
+                                            int bb, const Col& col, float u, unsigned long long* overflow_acc) {
+  const int lane = a.lane;
   if (C.na >= MAXA) { (*overflow_acc)++; return; }
-  while (W.cur < W.nc_old && (int)(W.curh & 63u) < p) cache_age_current(S, L, lane, e, W, overflow_acc);
+  while (W.cur < W.nc_old && (int)(W.curh & 63u) < p) cache_age_current(a, L, W, overflow_acc);
   const bool found = W.cur < W.nc_old && (int)(W.curh & 63u) == p;
   const uint32_t oh = W.curh;
   float oj[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   if (found) {
-    const float4 j = old_imp(S, L, lane, e, W.par, W.cur);
+    const float4 j = old_imp(a, L, W.par, W.cur);
     oj[0] = j.x; oj[1] = j.y; oj[2] = j.z; oj[3] = j.w;
-    cache_advance(S, L, lane, e, W);
+    cache_advance(a, L, W);
   }
   int pos = W.out;
   if (W.out < MAXA) ++W.out; else { (*overflow_acc)++; pos = 63; }
@@ -751,13 +720,12 @@ __device__ __forceinline__ void add_arbiter(const DevState& S, int64_t e, const 
 }
 
 // cache entry of a touched arbiter from its first contact c0 (and c1 when it has two)
-__device__ __forceinline__ void write_arbiter_cache(const DevState& S, int npar, int64_t e, const CSlot& c0,
-                                                    const CSlot& c1) {
+__device__ __forceinline__ void write_arbiter_cache(At a, int npar, const CSlot& c0, const CSlot& c1) {
   if (CS_CIDX(c0.m) != 0 || CS_POS(c0.m) >= MAXA) return;
   const bool two = CS_COUNT(c0.m) > 1;
   const uint32_t hdr = (uint32_t)CS_PAIR(c0.m) | (CS_COUNT(c0.m) << 6) | (CS_HASH(c0.m) << 16) |
                        ((two ? CS_HASH(c1.m) : 0u) << 24);
-  cache_write(S, npar, CS_POS(c0.m), e, hdr, make_float4(c0.jn, c0.jt, two ? c1.jn : 0.0f, two ? c1.jt : 0.0f));
+  cache_write(a, npar, CS_POS(c0.m), hdr, make_float4(c0.jn, c0.jt, two ? c1.jn : 0.0f, two ? c1.jt : 0.0f));
 }
 
 #define FOR_CONTACTS(C, OVF, BODY)                                    \
@@ -775,9 +743,10 @@ __device__ __forceinline__ void write_arbiter_cache(const DevState& S, int npar,
     }                                                                 \
   }
 
-__device__ __forceinline__ void physics_step(const DevState& S, const Params& P, int64_t e, Env& E, float fx[4],
-                                             float fy[4], float tq[4], Lds& L, int lane,
-                                             unsigned long long* overflow_acc, Snap& h2) {
+__device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e, const Params& P, Env& E, float fx[4],
+                                             float fy[4], float tq[4], Lds& L, unsigned long long* overflow_acc,
+                                             Snap& h2) {
+  const int lane = a.lane;
   const float dt = P.dt;
   // cpBodyUpdatePosition
 #pragma unroll
@@ -832,9 +801,6 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     for (int s = 0; s < 6; ++s)
       if (bb_intersects(ballbb, P.seg[s].bb)) mBS |= 1u << s;
   }
-#if MS_ABLATE == 2
-  mAA = mBA = mSA = mBS = 0;
-#endif
 
   CSlot* ovf = (CSlot*)S.SP + e * (MAXC - KREG);
   Contacts C;
@@ -843,12 +809,9 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
   CacheWalk W;
   W.par = (E.meta & META_PAR) ? 1 : 0;
   W.nc_old = META_NC(E.meta);
-#if MS_ABLATE == 4  // old arbiter cache ignored (timing ablation)
-  W.nc_old = 0;
-#endif
   W.cur = 0;
   W.out = 0;
-  W.curh = W.nc_old > 0 ? old_hdr(S, L, lane, e, W.par, 0) : 0xffffffffu;
+  W.curh = W.nc_old > 0 ? old_hdr(a, L, W.par, 0) : 0xffffffffu;
 
   // narrowphase, one compacted loop per pair class so each lane visits only its own touching
   // pairs; class order + ctz order = canonical pair order (DESIGN.md pair table)
@@ -862,7 +825,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     lds_box(L, j, lane, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     col_box_box(A, B, col);
-    if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, p, i, j, col, P.u_aa, overflow_acc);
+    if (col.count) add_arbiter(a, L, C, ovf, W, p, i, j, col, P.u_aa, overflow_acc);
   }
   while (mBA) {
     const int i = __builtin_ctz(mBA);
@@ -871,7 +834,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     lds_box(L, i, lane, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     col_circle_box(ballc, BR, B, col);
-    if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, 6 + i, 4, i, col, P.u_ab, overflow_acc);
+    if (col.count) add_arbiter(a, L, C, ovf, W, 6 + i, 4, i, col, P.u_ab, overflow_acc);
   }
   STAMP(11);
   while (mSA) {
@@ -883,7 +846,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     const Seg sg = L.seg[s];
     col_seg_box(sg, B, col);
-    if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, 10 + q, 5, i, col, s < 6 ? P.u_aw : P.u_ag, overflow_acc);
+    if (col.count) add_arbiter(a, L, C, ovf, W, 10 + q, 5, i, col, s < 6 ? P.u_aw : P.u_ag, overflow_acc);
   }
   STAMP(13);
   while (mBS) {
@@ -892,9 +855,9 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     const Seg sg = L.seg[s];
     col_circle_seg(ballc, BR, sg, col);
-    if (col.count) add_arbiter(S, e, L, lane, C, ovf, W, 42 + s, 4, 5, col, P.u_bw, overflow_acc);
+    if (col.count) add_arbiter(a, L, C, ovf, W, 42 + s, 4, 5, col, P.u_bw, overflow_acc);
   }
-  while (W.cur < W.nc_old) cache_age_current(S, L, lane, e, W, overflow_acc);
+  while (W.cur < W.nc_old) cache_age_current(a, L, W, overflow_acc);
   STAMP(3);
 #ifdef MS_STAMPS
   {
@@ -930,13 +893,13 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
   }
 
   STAMP(4);
-  if (MS_H2_AT == 1) snap_load(S, e, h2);  // arrives during the solver
+  if (!MS_EARLY_OBS) snap_load(a, h2);  // arrives during the solver
   if (C.nc > 0) {
     // cpArbiterApplyCachedImpulse, then cpArbiterApplyImpulse x 10 (pymunk Space default)
     FOR_CONTACTS(C, ovf, warm_one(P, c_, L, lane));
     STAMP(15);
 #pragma unroll 1
-    for (int it = 0; it < 10 * (MS_ABLATE != 1); ++it) {
+    for (int it = 0; it < 10; ++it) {
       asm volatile("; MS_SOLVER_ITER_BEGIN" ::: "memory");
       FOR_CONTACTS(C, ovf, solve_one(P, c_, L, lane));
       asm volatile("; MS_SOLVER_ITER_END" ::: "memory");
@@ -953,14 +916,17 @@ __device__ __forceinline__ void physics_step(const DevState& S, const Params& P,
     // touched arbiters' cache entries at the positions reserved in merge order
     static_for<0, KREG - 1>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
-      if (k < C.nc) write_arbiter_cache(S, W.par ^ 1, e, C.reg[k], C.reg[k + 1]);
+      if (k < C.nc) write_arbiter_cache(a, W.par ^ 1, C.reg[k], C.reg[k + 1]);
     });
     if (KREG - 1 < C.nc) {
       CSlot next = C.reg[KREG - 1];
       if (KREG < C.nc) next = ovf[0];
-      write_arbiter_cache(S, W.par ^ 1, e, C.reg[KREG - 1], next);
+      write_arbiter_cache(a, W.par ^ 1, C.reg[KREG - 1], next);
     }
-    for (int k = KREG; k < C.nc; ++k) write_arbiter_cache(S, W.par ^ 1, e, ovf[k - KREG], ovf[k + 1 - KREG]);
+    // the contact after the last one is never read (count > 1 only for an arbiter's first contact,
+    // whose second contact exists); k + 1 stays inside the env's spill slice
+    for (int k = KREG; k < C.nc; ++k)
+      write_arbiter_cache(a, W.par ^ 1, ovf[k - KREG], ovf[k + 1 < MAXC ? k + 1 - KREG : k - KREG]);
   }
   STAMP(6);
   const int nn = W.out < MAXA ? W.out : MAXA;
@@ -975,9 +941,9 @@ __device__ __forceinline__ void unpack_scalars(int4 v, Env& E) {
   E.meta = (uint32_t)v.z;
   E.rng.u32 = (uint32_t)v.w;
 }
-__device__ __forceinline__ void load_scalars(const DevState& S, int64_t e, Env& E) { unpack_scalars(S.I4[e], E); }
-__device__ __forceinline__ void store_scalars(const DevState& S, int64_t e, const Env& E) {
-  S.I4[e] = make_int4(E.steps, (int32_t)(((uint32_t)E.score_blue & 0xffffu) | ((uint32_t)E.score_red << 16)),
+__device__ __forceinline__ void load_scalars(At a, Env& E) { unpack_scalars(*plane<int4>(a, OFF_I4, 0), E); }
+__device__ __forceinline__ void store_scalars(At a, const Env& E) {
+  *plane<int4>(a, OFF_I4, 0) = make_int4(E.steps, (int32_t)(((uint32_t)E.score_blue & 0xffffu) | ((uint32_t)E.score_red << 16)),
                       (int32_t)E.meta, (int32_t)E.rng.u32);
 }
 
@@ -1025,33 +991,30 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   __shared__ Lds L;
   STAMP(0);
   const int lane = threadIdx.x;
-  const int64_t e0 = (int64_t)blockIdx.x * MS_BLOCK;
-  const int64_t e = e0 + lane;
+  const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + lane;
   bool active = e < S.n;
+  // the wave's state block: a wave-uniform base (blockIdx.x) and this lane's slot in it
+  const At at{S.blocks + (int64_t)blockIdx.x * BLOCK_BYTES, lane};
 
-  // (1) loads, in the order their data is needed. They are unconditional (an inactive lane
-  // reads env n-1): loads under a lane branch make the compiler copy the loaded registers at
-  // the join, and every copy waits for its load.
-  const int64_t el = active ? e : S.n - 1;
+  // (1) loads, in the order their data is needed. They are unconditional (a padding lane of the
+  // last block reads its zeroed slot and the last env's actions): loads under a lane branch make
+  // the compiler copy the loaded registers at the join, and every copy waits for its load.
   Env E;
-  unpack_scalars(S.I4[el], E);
-  load_bodies(S, el, E);
+  load_scalars(at, E);
+  load_bodies(at, E);
   Snap h2;  // obs-history snapshot t-2
-  if (MS_ABLATE != 6 && (MS_H2_AT == 0 || MS_H2_AT == 4)) snap_load(S, el, h2);
+  if (MS_EARLY_OBS) snap_load(at, h2);
   float a[12];
   {
-    const float4* ap = (const float4*)(actions + el * 12);
+    const float4* ap = (const float4*)(actions + (active ? e : S.n - 1) * 12);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       const float4 v = ap[q];
       a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
     }
   }
-  int nco = META_NC(E.meta);
+  const int nco = META_NC(E.meta);
   const int par0 = (E.meta & META_PAR) ? 1 : 0;
-#if MS_ABLATE == 4  // old arbiter cache ignored (timing ablation)
-  nco = 0;
-#endif
   // old arbiter cache entries k < KC. No branch (so the compiler's wait counts stay exact): a
   // lane without entry k re-reads its own scalars/bodies, which are in L1, instead.
   uint32_t pch[KC];
@@ -1059,9 +1022,8 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
     const bool need = k < nco;
-    const int64_t o = (int64_t)(par0 * MAXA + k) * S.n + el;
-    const uint32_t* hp = need ? &S.CH[o] : (const uint32_t*)&S.I4[el];
-    const float4* jp = need ? &S.CJ[o] : &S.B4[el];
+    const uint32_t* hp = need ? plane<uint32_t>(at, OFF_CH, par0 * MAXA + k) : (const uint32_t*)plane<int4>(at, OFF_I4, 0);
+    const float4* jp = need ? plane<float4>(at, OFF_CJ, par0 * MAXA + k) : plane<float4>(at, OFF_B4, 0);
     pch[k] = *hp;
     pcj[k] = *jp;
   }
@@ -1069,13 +1031,10 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   for (int k = 0; k < KC; ++k) { L.ch[k][lane] = pch[k]; L.cj[k][lane] = pcj[k]; }
 
   stage_segments(P, L, lane);
-  bool fill3 = false, rng_loaded = false, rng_dirty = false;
-#if MS_RNG_EARLY
+  bool fill3 = false, rng_dirty = false;
   // PCG64 for goal respawns and auto-resets, with the first batch for every lane: 32 B/env
   // more in the start burst instead of a dependent HBM round trip in most waves
-  load_rng(S, el, E);
-  rng_loaded = true;
-#endif
+  load_rng(at, E);
   Snap h1;  // obs-history snapshot t-1: the body state before this step
   if (active) {
     // SoccerEnv.step validation (soccer_env.py:101-117): a non-finite action skips the env
@@ -1094,22 +1053,27 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   if (active) {
     E.steps += 1;
     const bool done_now = P.max_steps > 0 && E.steps >= P.max_steps;
-#if !MS_RNG_EARLY
-    // PCG64 state now if this step may respawn (ball within 30 px of a goal mouth — it moves
-    // <= 4 px per step — or the episode ends here)
-    if (((E.px[4] < 40.0f || E.px[4] > 760.0f) && E.py[4] > 195.0f && E.py[4] < 405.0f) || (P.autoreset && done_now)) {
-      load_rng(S, e, E);
-      rng_loaded = true;
-    }
-#endif
     // the stack is refilled instead of shifted after a reset (hist_empty) or an auto-reset at
     // the end of this step
     fill3 = (E.meta & META_HE) != 0 || (P.autoreset && done_now);
     snap_of(E, h1);
-#if MS_H2_AT == 4
-    snap_to_lds(L.h2, lane, h2);
-#endif
-#if MS_H1_LDS
+#if MS_EARLY_OBS
+    // frames t-2 and t-1 and the history slot do not depend on this step's physics: stored now,
+    // while the physics runs (a refilled stack writes three copies of frame t at the end instead)
+    if (!fill3) {
+      if (obs) emit_two(P, h2, h1, obs + e * 264);
+      snap_store(at, h1);  // t-1 becomes the next step's t-2
+    }
+    {
+      // step-start positions (the reward's previous state) staged in LDS across the physics
+      float f[12];
+#pragma unroll
+      for (int b = 0; b < 5; ++b) { f[b] = h1.px[b]; f[5 + b] = h1.py[b]; }
+      f[10] = 0.0f; f[11] = 0.0f;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) L.h1[g][lane] = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
+    }
+#else
     snap_to_lds(L.h1, lane, h1);  // back at the end: not held in registers across the physics
 #endif
   }
@@ -1137,19 +1101,25 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
 
     unsigned long long ovf = 0;
     STAMP(1);
-    physics_step(S, P, e, E, fx, fy, tq, L, lane, &ovf, h2);
-    if (MS_H2_AT == 2) snap_load(S, e, h2);
-#if MS_H2_AT == 4
-    snap_from_lds(L.h2, lane, h2);
-#endif
-#if MS_P_RELOAD  // positions back from LDS (written by the position phase, unchanged since)
+    physics_step(S, at, e, P, E, fx, fy, tq, L, &ovf, h2);
+    // positions back from LDS (written by the position phase, unchanged since)
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
       const V2 p = L.ph.p[b][lane];
       E.px[b] = p.x; E.py[b] = p.y;
     }
-#endif
-#if MS_H1_LDS
+#if MS_EARLY_OBS
+    {
+      float f[12];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        const float4 v = L.h1[g][lane];
+        f[4 * g] = v.x; f[4 * g + 1] = v.y; f[4 * g + 2] = v.z; f[4 * g + 3] = v.w;
+      }
+#pragma unroll
+      for (int b = 0; b < 5; ++b) { pvx[b] = f[b]; pvy[b] = f[5 + b]; }
+    }
+#else
     snap_from_lds(L.h1, lane, h1);
 #pragma unroll
     for (int b = 0; b < 5; ++b) { pvx[b] = h1.px[b]; pvy[b] = h1.py[b]; }
@@ -1165,7 +1135,6 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     const bool done = P.max_steps > 0 && E.steps >= P.max_steps;
     float r = blue_reward(P, pvx, pvy, E.px, E.py, goal, false, 0, 0);
     if (goal) {
-      if (!rng_loaded) load_rng(S, e, E);
       rng_dirty = true;
       soft_reset_regs(E);
     }
@@ -1180,7 +1149,6 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
 
     if (done && P.autoreset) {
       // marl_vecenv.py:48-51: env.reset(options={"use_full_random_positions": True})
-      if (!rng_dirty && !rng_loaded) load_rng(S, e, E);
       rng_dirty = true;
       reset_env_regs(E, MS_SPAWN_FULL_RANDOM);
     }
@@ -1191,18 +1159,18 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     Snap s0;
     snap_of(E, s0);
     if (fill3) {
-      emit_fill3(S, P, e, s0, obs);
+      emit_fill3(at, P, e, s0, obs);
       E.meta &= ~META_HE;
-    } else if (MS_ABLATE == 6) {  // frame t only, no history traffic (timing ablation)
-      if (obs) emit_snapshot<2>(P, s0, obs + e * 264);
+    } else if (MS_EARLY_OBS) {
+      if (obs) emit_snapshot<2>(P, s0, obs + e * 264);  // frame t; t-2, t-1 went out before the physics
     } else {
-      if (obs && MS_ABLATE != 3) emit_three(P, h2, h1, s0, obs + e * 264);
-      snap_store(S, e, h1);  // t-1 becomes the next step's t-2
+      if (obs) emit_three(P, h2, h1, s0, obs + e * 264);
+      snap_store(at, h1);  // t-1 becomes the next step's t-2
     }
     STAMP(9);
-    if (rng_dirty) store_rng(S, e, E);
-    store_bodies(S, e, E);
-    store_scalars(S, e, E);
+    if (rng_dirty) store_rng(at, E);
+    store_bodies(at, E);
+    store_scalars(at, E);
   }
   STAMP(10);
 }
@@ -1229,32 +1197,34 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_reset_kernel(DevState S, Params P
   const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + threadIdx.x;
   const bool active = e < S.n && (!mask || mask[e]);
   if (!active) return;
+  const At a = env_at(S, e);
   Env E;
-  load_scalars(S, e, E);
+  load_scalars(a, E);
   if (pcg) {
     E.rng.shi = pcg[e * 4 + 0]; E.rng.slo = pcg[e * 4 + 1];
     E.rng.ihi = pcg[e * 4 + 2]; E.rng.ilo = pcg[e * 4 + 3];
     E.rng.has32 = 0; E.rng.u32 = 0;
   } else {
-    load_rng(S, e, E);
+    load_rng(a, E);
   }
   reset_env_regs(E, mode);
   Snap s0;
   snap_of(E, s0);
-  emit_fill3(S, P, e, s0, obs);
+  emit_fill3(a, P, e, s0, obs);
   E.meta &= ~META_HE;
   if (set_hist_empty) E.meta |= META_HE;
-  store_rng(S, e, E);
-  store_bodies(S, e, E);
-  store_scalars(S, e, E);
+  store_rng(a, E);
+  store_bodies(a, E);
+  store_scalars(a, E);
 }
 
 __global__ __launch_bounds__(MS_BLOCK) void ms_observe_kernel(DevState S, Params P, float* __restrict__ frames) {
   const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + threadIdx.x;
   if (e >= S.n) return;
+  const At a = env_at(S, e);
   Env E;
-  load_scalars(S, e, E);
-  load_bodies(S, e, E);
+  load_scalars(a, E);
+  load_bodies(a, E);
 #pragma unroll 1
   for (int a = 0; a < 4; ++a) {
     float f[22];
@@ -1267,10 +1237,11 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_observe_kernel(DevState S, Params
 __global__ void ms_export_kernel(DevState S, ms_env_state* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= S.n) return;
+  const At a = env_at(S, e);
   Env E;
-  load_scalars(S, e, E);
-  load_bodies(S, e, E);
-  load_rng(S, e, E);
+  load_scalars(a, E);
+  load_bodies(a, E);
+  load_rng(a, E);
   ms_env_state& o = out[e];
   for (int b = 0; b < 5; ++b) {
     ms_body_state& d = o.body[b];
@@ -1279,7 +1250,7 @@ __global__ void ms_export_kernel(DevState S, ms_env_state* __restrict__ out) {
     d.w = E.w[b]; d.vbx = E.vbx[b]; d.vby = E.vby[b]; d.wb = E.wb[b];
   }
   Snap h2, h1;
-  snap_load(S, e, h2);
+  snap_load(a, h2);
   snap_of(E, h1);  // the t-1 snapshot is the current body state
   for (int b = 0; b < 5; ++b) {
     o.snap[0][b] = h2.px[b]; o.snap[0][5 + b] = h2.py[b];
@@ -1304,10 +1275,10 @@ __global__ void ms_export_kernel(DevState S, ms_env_state* __restrict__ out) {
     ms_arbiter_state& A = o.arb[k];
     memset(&A, 0, sizeof(A));
     if (k >= nc) continue;
-    const uint32_t h = S.CH[(int64_t)(par * MAXA + k) * S.n + e];
+    const uint32_t h = *plane<uint32_t>(a, OFF_CH, par * MAXA + k);
     A.pair = h & 63u; A.count = (h >> 6) & 3u; A.idle = (h >> 8) & 3u;
     A.hash[0] = (h >> 16) & 0xffu; A.hash[1] = (h >> 24) & 0xffu;
-    const float4 j = S.CJ[(int64_t)(par * MAXA + k) * S.n + e];
+    const float4 j = *plane<float4>(a, OFF_CJ, par * MAXA + k);
     A.jn[0] = j.x; A.jt[0] = j.y; A.jn[1] = j.z; A.jt[1] = j.w;
   }
 }
@@ -1317,6 +1288,7 @@ __global__ void ms_export_kernel(DevState S, ms_env_state* __restrict__ out) {
 __global__ void ms_import_kernel(DevState S, const ms_env_state* __restrict__ in) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= S.n) return;
+  const At a = env_at(S, e);
   const ms_env_state& o = in[e];
   Env E;
   for (int b = 0; b < 5; ++b) {
@@ -1335,16 +1307,16 @@ __global__ void ms_import_kernel(DevState S, const ms_env_state* __restrict__ in
   for (int i = 0; i < 4; ++i) {
     h2.vx[i] = o.snap[0][10 + i]; h2.vy[i] = o.snap[0][14 + i]; h2.ang[i] = o.snap[0][18 + i]; h2.w[i] = o.snap[0][22 + i];
   }
-  snap_store(S, e, h2);
+  snap_store(a, h2);
   for (int k = 0; k < nc; ++k) {
     const ms_arbiter_state& A = o.arb[k];
-    S.CH[(int64_t)k * S.n + e] = (uint32_t)(A.pair & 63u) | ((uint32_t)(A.count & 3u) << 6) |
+    *plane<uint32_t>(a, OFF_CH, k) = (uint32_t)(A.pair & 63u) | ((uint32_t)(A.count & 3u) << 6) |
                                  ((uint32_t)(A.idle & 3u) << 8) | ((uint32_t)A.hash[0] << 16) | ((uint32_t)A.hash[1] << 24);
-    S.CJ[(int64_t)k * S.n + e] = make_float4(A.jn[0], A.jt[0], A.jn[1], A.jt[1]);
+    *plane<float4>(a, OFF_CJ, k) = make_float4(A.jn[0], A.jt[0], A.jn[1], A.jt[1]);
   }
-  store_rng(S, e, E);
-  store_bodies(S, e, E);
-  store_scalars(S, e, E);
+  store_rng(a, E);
+  store_bodies(a, E);
+  store_scalars(a, E);
 }
 
 __global__ void ms_debug_rewards_kernel(Params P, int64_t n, const float* __restrict__ prev, const float* __restrict__ cur,
@@ -1559,25 +1531,14 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
   make_params(&h->cfg, &h->P);
   h->default_params = params_are_default(h->P);
   const size_t n = (size_t)n_envs;
-  const size_t bytes_B = sizeof(float4) * G_BODY * n;
-  const size_t bytes_H = sizeof(float4) * G_SNAP * n;
-  const size_t bytes_I = sizeof(int4) * n;
-  const size_t bytes_R = sizeof(ulonglong2) * 2 * n;
-  const size_t bytes_CH = sizeof(uint32_t) * 2 * MAXA * n;
-  const size_t bytes_CJ = sizeof(float4) * 2 * MAXA * n;
-  const size_t total = bytes_R + bytes_B + bytes_H + bytes_I + bytes_CJ + bytes_CH + 256;
+  const size_t total = (size_t)((n + BLK - 1) / BLK) * BLOCK_BYTES;  // state blocks, the last one padded
   char* base = nullptr;
   if (hipMalloc((void**)&base, total) != hipSuccess) {
     delete h;
     return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of device state failed");
   }
   h->mem = base;
-  h->S.R2 = (ulonglong2*)base; base += bytes_R;
-  h->S.B4 = (float4*)base; base += bytes_B;
-  h->S.H4 = (float4*)base; base += bytes_H;
-  h->S.I4 = (int4*)base; base += bytes_I;
-  h->S.CJ = (float4*)base; base += bytes_CJ;
-  h->S.CH = (uint32_t*)base; base += bytes_CH;
+  h->S.blocks = base;
   h->S.n = n_envs;
   h->S.stamps = nullptr;
   // contact-slot spill for pile-ups beyond KREG contacts: reserved address space, touched
