@@ -386,8 +386,40 @@ __device__ __forceinline__ void col_seg_box(const Seg& s, const Box& bx, Col& co
     float best = __builtin_inff();
     V2 pa = v2(0.0f, 0.0f), pb = v2(0.0f, 0.0f), fn = v2(0.0f, 0.0f);
     int kind = 0;
+    // The sequential minimum below keeps the first candidate of the smallest d2 (endpoint
+    // candidates first, then box vertices). The vertex candidates are evaluated first here;
+    // an endpoint whose distance to the box's bounding box exceeds the best vertex distance
+    // by more than 0.5 (far above the fp32 rounding of any candidate's d2) cannot be that
+    // minimum, so its four edge candidates are skipped. Same winner, same bits.
+    float bestV = __builtin_inff();
+    V2 paV = pa, pbV = pb, fnV = fn;
+    int kindV = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      V2 a = vsub(sa, bx.v[j]), b = vsub(sb, bx.v[j]);
+      float t = closest_t(a, b);
+      V2 p = lerp_t(a, b, t);
+      float d2 = vlengthsq(p);
+      if (d2 < bestV) {
+        bestV = d2; paV = lerp_t(sa, sb, t); pbV = bx.v[j];
+        if (t > -1.0f && t < 1.0f) {
+          kindV = 1;
+          fnV = (vdot(sn, vsub(bx.v[j], sa)) > 0.0f) ? sn : vneg(sn);
+        } else kindV = 0;
+      }
+    }
+    const float reach = __builtin_amdgcn_sqrtf(bestV) + 0.5f;
+    bool need[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
+      const V2 e = k == 0 ? sa : sb;
+      const float dx = fmaxf(fmaxf(bx.bb[0] - e.x, e.x - bx.bb[2]), 0.0f);
+      const float dy = fmaxf(fmaxf(bx.bb[1] - e.y, e.y - bx.bb[3]), 0.0f);
+      need[k] = !(dx * dx + dy * dy > reach * reach);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (!need[k]) continue;
       V2 e = k == 0 ? sa : sb;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -402,20 +434,7 @@ __device__ __forceinline__ void col_seg_box(const Seg& s, const Box& bx, Col& co
         }
       }
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      V2 a = vsub(sa, bx.v[j]), b = vsub(sb, bx.v[j]);
-      float t = closest_t(a, b);
-      V2 p = lerp_t(a, b, t);
-      float d2 = vlengthsq(p);
-      if (d2 < best) {
-        best = d2; pa = lerp_t(sa, sb, t); pb = bx.v[j];
-        if (t > -1.0f && t < 1.0f) {
-          kind = 1;
-          fn = (vdot(sn, vsub(bx.v[j], sa)) > 0.0f) ? sn : vneg(sn);
-        } else kind = 0;
-      }
-    }
+    if (bestV < best) { best = bestV; pa = paV; pb = pbV; fn = fnV; kind = kindV; }
     V2 p = vsub(pb, pa);
     if (kind) {
       n = fn;

@@ -67,7 +67,7 @@ constexpr int OFF_CJ = OFF_CH + 2 * MAXA * BLK * 4;
 constexpr int BLOCK_BYTES = OFF_CJ + 2 * MAXA * BLK * 16;
 
 struct DevState {
-  unsigned long long* stamps;  // MS_STAMPS diagnostic builds only: [wave][16] s_memtime
+  unsigned long long* stamps;  // MS_STAMPS diagnostic builds only: [wave][MS_NSTAMP] s_memtime
   char* blocks;                // [ceil(n / 64)] state blocks
   void* SP;  // contact slots KREG.. of each env (pile-ups only): [env][MAXC - KREG] CSlot
   int64_t n;
@@ -104,11 +104,32 @@ struct Counters {
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
     const unsigned long long act_ = __ballot(1);                                          \
     if ((int)(threadIdx.x & 63) == __ffsll((long long)act_) - 1 && S.stamps)              \
-      S.stamps[(int64_t)(blockIdx.x) * 16 + (k)] = t_;                                   \
+      S.stamps[(int64_t)(blockIdx.x) * MS_NSTAMP + (k)] = t_;                                   \
+  } while (0)
+// cycles spent inside a region of a divergent loop, accumulated per lane; the wave's figure is
+// the maximum over its lanes (the lane that ran the most iterations), written to slot k
+#define ACC_DECL(v) unsigned long long v = 0
+#define ACC_BEGIN(v) const unsigned long long v##_t0 = __builtin_amdgcn_s_memtime()
+#define ACC_END(v) v += __builtin_amdgcn_s_memtime() - v##_t0
+#define ACC_INC(v) v++
+#define ACC_STORE(v, k)                                                                    \
+  do {                                                                                   \
+    unsigned long long m_ = v;                                                           \
+    for (int o_ = 32; o_ > 0; o_ >>= 1) {                                                \
+      const unsigned long long x_ = __shfl_xor(m_, o_);                                  \
+      m_ = x_ > m_ ? x_ : m_;                                                            \
+    }                                                                                    \
+    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[(int64_t)blockIdx.x * MS_NSTAMP + (k)] = m_; \
   } while (0)
 #else
 #define STAMP(k) do { } while (0)
+#define ACC_DECL(v) do { } while (0)
+#define ACC_BEGIN(v) do { } while (0)
+#define ACC_END(v) do { } while (0)
+#define ACC_INC(v) do { } while (0)
+#define ACC_STORE(v, k) do { } while (0)
 #endif
+#define MS_NSTAMP 24
 
 // ---- per-lane env register file ------------------------------------------------------------
 struct Env {
@@ -177,7 +198,11 @@ enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
 #define MS_EARLY_OBS 0  // 1: frames t-2, t-1 and the history slot stored before the physics
 #endif
 
-constexpr int KC = 4;  // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (rare)
+#ifndef MS_KC
+#define MS_KC 8
+#endif
+constexpr int KC = MS_KC;   // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (never seen)
+constexpr int KC0 = 4;  // entries loaded by every wave; KC0..KC-1 only by waves where some lane has them
 
 struct Lds {
   Seg seg[8];  // static segments (walls, goal lines), read with per-lane indices
@@ -640,11 +665,15 @@ __device__ __forceinline__ void lds_box(const Lds& L, int i, int lane, Box& b) {
 
 // Old-cache cursor: the previous step's arbiter cache (sorted by pair id) is streamed once,
 // merged with this step's touched arbiters into the other (ping-pong) buffer. Entries below KC
-// come from LDS (staged at kernel start), the rest from HBM.
+// come from LDS (staged at kernel start), the rest from HBM. The cursor decisions (pair id and
+// idle count of the entry under it) come from one key byte per entry packed into two registers
+// at the load, so advancing the cursor never waits for an LDS read; the full header and the
+// impulses are read only for an entry that is aged or matched.
 struct CacheWalk {
   int par, nc_old, cur, out;
-  uint32_t curh;
+  uint32_t pk[2];  // key bytes (pair | idle << 6) of entries 0..7
 };
+__device__ __forceinline__ uint32_t cache_key(uint32_t hdr) { return (hdr & 63u) | (((hdr >> 8) & 3u) << 6); }
 
 // (the HBM fallback reads through address-space-1 pointers: with generic pointers the optimizer
 // merges the LDS and the global read into one flat-address load through a selected address)
@@ -659,23 +688,29 @@ __device__ __forceinline__ float4 old_imp(At a, const Lds& L, int par, int k) {
                      __uint_as_float(__builtin_nontemporal_load(g + 2)), __uint_as_float(__builtin_nontemporal_load(g + 3)));
 }
 
-__device__ __forceinline__ void cache_advance(At a, const Lds& L, CacheWalk& W) {
-  ++W.cur;
-  W.curh = W.cur < W.nc_old ? old_hdr(a, L, W.par, W.cur) : 0xffffffffu;
+// key byte of the entry under the cursor (cur < nc_old)
+__device__ __forceinline__ uint32_t cur_key(At a, const CacheWalk& W) {
+  if (W.cur < KC) return ((W.cur < 4 ? W.pk[0] : W.pk[1]) >> (8 * (W.cur & 3))) & 0xffu;
+  return cache_key(__builtin_nontemporal_load((gu32_t*)plane<uint32_t>(a, OFF_CH, W.par * MAXA + W.cur)));
+}
+// pair id under the cursor, 64 past the end of the old cache
+__device__ __forceinline__ int cur_pair(At a, const CacheWalk& W) {
+  return W.cur < W.nc_old ? (int)(cur_key(a, W) & 63u) : 64;
 }
 
 // emit the old entry under the cursor aged by one step (dropped at idle 3, cpSpaceArbiterSetFilter)
 __device__ __forceinline__ void cache_age_current(At a, const Lds& L, CacheWalk& W, unsigned long long* overflow_acc) {
-  const uint32_t idle = ((W.curh >> 8) & 3u) + 1u;
+  const uint32_t idle = (cur_key(a, W) >> 6) + 1u;
   if (idle < 3u) {
     if (W.out < MAXA) {
-      cache_write(a, W.par ^ 1, W.out, (W.curh & ~(3u << 8)) | (idle << 8), old_imp(a, L, W.par, W.cur));
+      const uint32_t h = old_hdr(a, L, W.par, W.cur);
+      cache_write(a, W.par ^ 1, W.out, (h & ~(3u << 8)) | (idle << 8), old_imp(a, L, W.par, W.cur));
       ++W.out;
     } else {
       (*overflow_acc)++;
     }
   }
-  cache_advance(a, L, W);
+  ++W.cur;
 }
 
 // cpSpaceCollideShapes + cpArbiterUpdate for one touching pair
@@ -683,40 +718,45 @@ __device__ __forceinline__ void add_arbiter(At a, const Lds& L, Contacts& C, CSl
                                             int bb, const Col& col, float u, unsigned long long* overflow_acc) {
   const int lane = a.lane;
   if (C.na >= MAXA) { (*overflow_acc)++; return; }
-  while (W.cur < W.nc_old && (int)(W.curh & 63u) < p) cache_age_current(a, L, W, overflow_acc);
-  const bool found = W.cur < W.nc_old && (int)(W.curh & 63u) == p;
-  const uint32_t oh = W.curh;
+  while (cur_pair(a, W) < p) cache_age_current(a, L, W, overflow_acc);
+  const bool found = cur_pair(a, W) == p;
+  uint32_t oh = 0u;
   float oj[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   if (found) {
+    oh = old_hdr(a, L, W.par, W.cur);
     const float4 j = old_imp(a, L, W.par, W.cur);
     oj[0] = j.x; oj[1] = j.y; oj[2] = j.z; oj[3] = j.w;
-    cache_advance(a, L, W);
+    ++W.cur;
   }
   int pos = W.out;
   if (W.out < MAXA) ++W.out; else { (*overflow_acc)++; pos = 63; }
   C.na++;
   const V2 pa = L.ph.p[ba][lane], pb = L.ph.p[bb][lane];
   const uint32_t warm = (found && ((oh >> 8) & 3u) == 0u) ? 1u : 0u;
-  for (int k = 0; k < col.count; ++k) {
-    CSlot s;
-    const V2 p1 = k == 0 ? col.p1[0] : col.p1[1];
-    const V2 p2 = k == 0 ? col.p2[0] : col.p2[1];
-    const int h = k == 0 ? col.hash[0] : col.hash[1];
-    s.r1 = vsub(p1, pa);
-    s.r2 = vsub(p2, pb);
-    s.n = col.n; s.u = u;
-    s.nMass = 0.0f; s.tMass = 0.0f; s.bias = 0.0f; s.bounce = 0.0f; s.jb = 0.0f;
-    s.jn = 0.0f; s.jt = 0.0f;
-    if (found) {
-      const int ocount = (oh >> 6) & 3u;
-      for (int j = 0; j < ocount; ++j)
-        if ((int)((oh >> (16 + 8 * j)) & 0xffu) == h) { s.jn = oj[2 * j]; s.jt = oj[2 * j + 1]; }
+  // the old arbiter's contact hashes (cpArbiterUpdate matches contacts by feature hash; a later
+  // old contact wins, as in the loop over the old contact list)
+  const int ocount = found ? (int)((oh >> 6) & 3u) : 0;
+  const int oh0 = (int)((oh >> 16) & 0xffu), oh1 = (int)((oh >> 24) & 0xffu);
+  // the one or two contacts of the collision, unrolled (no loop control in the hot path)
+  static_for<0, 2>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    if (k == 0 || col.count > 1) {
+      CSlot s;
+      const int h = col.hash[k];
+      s.r1 = vsub(col.p1[k], pa);
+      s.r2 = vsub(col.p2[k], pb);
+      s.n = col.n; s.u = u;
+      s.nMass = 0.0f; s.tMass = 0.0f; s.bias = 0.0f; s.bounce = 0.0f; s.jb = 0.0f;
+      float jn = 0.0f, jt = 0.0f;
+      if (ocount > 0 && oh0 == h) { jn = oj[0]; jt = oj[1]; }
+      if (ocount > 1 && oh1 == h) { jn = oj[2]; jt = oj[3]; }
+      s.jn = jn; s.jt = jt;
+      s.m = (uint32_t)ba | ((uint32_t)bb << 3) | (warm << 6) | ((uint32_t)k << 7) | ((uint32_t)col.count << 8) |
+            ((uint32_t)(h & 0xff) << 10) | ((uint32_t)pos << 18) | ((uint32_t)p << 24);
+      slot_put(C, ovf, C.nc + k, s);
     }
-    s.m = (uint32_t)ba | ((uint32_t)bb << 3) | (warm << 6) | ((uint32_t)k << 7) | ((uint32_t)col.count << 8) |
-          ((uint32_t)(h & 0xff) << 10) | ((uint32_t)pos << 18) | ((uint32_t)p << 24);
-    slot_put(C, ovf, C.nc, s);
-    C.nc++;
-  }
+  });
+  C.nc += col.count;
 }
 
 // cache entry of a touched arbiter from its first contact c0 (and c1 when it has two)
@@ -745,7 +785,7 @@ __device__ __forceinline__ void write_arbiter_cache(At a, int npar, const CSlot&
 
 __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e, const Params& P, Env& E, float fx[4],
                                              float fy[4], float tq[4], Lds& L, unsigned long long* overflow_acc,
-                                             Snap& h2) {
+                                             Snap& h2, uint32_t pk0, uint32_t pk1) {
   const int lane = a.lane;
   const float dt = P.dt;
   // cpBodyUpdatePosition
@@ -811,8 +851,13 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
   W.nc_old = META_NC(E.meta);
   W.cur = 0;
   W.out = 0;
-  W.curh = W.nc_old > 0 ? old_hdr(a, L, W.par, 0) : 0xffffffffu;
+  W.pk[0] = pk0;
+  W.pk[1] = pk1;
 
+  ACC_DECL(aa_col); ACC_DECL(aa_add); ACC_DECL(sa_col); ACC_DECL(sa_add);
+#ifdef MS_STAMPS
+  unsigned long long aa_n = 0, sa_n = 0;
+#endif
   // narrowphase, one compacted loop per pair class so each lane visits only its own touching
   // pairs; class order + ctz order = canonical pair order (DESIGN.md pair table)
   while (mAA) {
@@ -824,8 +869,13 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     lds_box(L, i, lane, A);
     lds_box(L, j, lane, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
+    ACC_BEGIN(aa_col);
     col_box_box(A, B, col);
+    ACC_END(aa_col);
+    ACC_BEGIN(aa_add);
     if (col.count) add_arbiter(a, L, C, ovf, W, p, i, j, col, P.u_aa, overflow_acc);
+    ACC_END(aa_add);
+    ACC_INC(aa_n);
   }
   while (mBA) {
     const int i = __builtin_ctz(mBA);
@@ -845,8 +895,13 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     lds_box(L, i, lane, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     const Seg sg = L.seg[s];
+    ACC_BEGIN(sa_col);
     col_seg_box(sg, B, col);
+    ACC_END(sa_col);
+    ACC_BEGIN(sa_add);
     if (col.count) add_arbiter(a, L, C, ovf, W, 10 + q, 5, i, col, s < 6 ? P.u_aw : P.u_ag, overflow_acc);
+    ACC_END(sa_add);
+    ACC_INC(sa_n);
   }
   STAMP(13);
   while (mBS) {
@@ -860,10 +915,12 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
   while (W.cur < W.nc_old) cache_age_current(a, L, W, overflow_acc);
   STAMP(3);
 #ifdef MS_STAMPS
+  ACC_STORE(aa_col, 16); ACC_STORE(aa_add, 17); ACC_STORE(aa_n, 18);
+  ACC_STORE(sa_col, 19); ACC_STORE(sa_add, 20); ACC_STORE(sa_n, 21);
   {
     int mx = C.nc;
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[(int64_t)blockIdx.x * 16 + 12] = (unsigned long long)mx;
+    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[(int64_t)blockIdx.x * MS_NSTAMP + 12] = (unsigned long long)mx;
   }
 #endif
 
@@ -1015,20 +1072,44 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   }
   const int nco = META_NC(E.meta);
   const int par0 = (E.meta & META_PAR) ? 1 : 0;
-  // old arbiter cache entries k < KC. No branch (so the compiler's wait counts stay exact): a
+  // old arbiter cache entries k < KC0. No branch (so the compiler's wait counts stay exact): a
   // lane without entry k re-reads its own scalars/bodies, which are in L1, instead.
-  uint32_t pch[KC];
-  float4 pcj[KC];
+  uint32_t pch[KC0];
+  float4 pcj[KC0];
 #pragma unroll
-  for (int k = 0; k < KC; ++k) {
+  for (int k = 0; k < KC0; ++k) {
     const bool need = k < nco;
     const uint32_t* hp = need ? plane<uint32_t>(at, OFF_CH, par0 * MAXA + k) : (const uint32_t*)plane<int4>(at, OFF_I4, 0);
     const float4* jp = need ? plane<float4>(at, OFF_CJ, par0 * MAXA + k) : plane<float4>(at, OFF_B4, 0);
     pch[k] = *hp;
     pcj[k] = *jp;
   }
+  uint32_t pk0 = 0u, pk1 = 0u;
 #pragma unroll
-  for (int k = 0; k < KC; ++k) { L.ch[k][lane] = pch[k]; L.cj[k][lane] = pcj[k]; }
+  for (int k = 0; k < KC0; ++k) {
+    L.ch[k][lane] = pch[k];
+    L.cj[k][lane] = pcj[k];
+    pk0 |= cache_key(pch[k]) << (8 * k);
+  }
+  // entries KC0..KC-1 (pile-ups: a few % of the waves) under a wave-uniform branch
+  if (KC > KC0 && __ballot(nco > KC0) != 0ull) {
+    uint32_t qch[KC > KC0 ? KC - KC0 : 1];
+    float4 qcj[KC > KC0 ? KC - KC0 : 1];
+#pragma unroll
+    for (int k = KC0; k < KC; ++k) {
+      const bool need = k < nco;
+      const uint32_t* hp = need ? plane<uint32_t>(at, OFF_CH, par0 * MAXA + k) : (const uint32_t*)plane<int4>(at, OFF_I4, 0);
+      const float4* jp = need ? plane<float4>(at, OFF_CJ, par0 * MAXA + k) : plane<float4>(at, OFF_B4, 0);
+      qch[k - KC0] = *hp;
+      qcj[k - KC0] = *jp;
+    }
+#pragma unroll
+    for (int k = KC0; k < KC; ++k) {
+      L.ch[k][lane] = qch[k - KC0];
+      L.cj[k][lane] = qcj[k - KC0];
+      pk1 |= cache_key(qch[k - KC0]) << (8 * (k - KC0));
+    }
+  }
 
   stage_segments(P, L, lane);
   bool fill3 = false, rng_dirty = false;
@@ -1101,7 +1182,7 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
 
     unsigned long long ovf = 0;
     STAMP(1);
-    physics_step(S, at, e, P, E, fx, fy, tq, L, &ovf, h2);
+    physics_step(S, at, e, P, E, fx, fy, tq, L, &ovf, h2, pk0, pk1);
     // positions back from LDS (written by the position phase, unchanged since)
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
@@ -1549,9 +1630,9 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
     return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of the contact spill buffer failed");
   }
 #ifdef MS_STAMPS
-  if (hipMalloc((void**)&h->S.stamps, sizeof(unsigned long long) * 16 * ((n + MS_BLOCK - 1) / MS_BLOCK)) != hipSuccess)
+  if (hipMalloc((void**)&h->S.stamps, sizeof(unsigned long long) * MS_NSTAMP * ((n + MS_BLOCK - 1) / MS_BLOCK)) != hipSuccess)
     return fail(MS_ERR_OUT_OF_MEMORY, "stamps");
-  (void)hipMemsetAsync(h->S.stamps, 0, sizeof(unsigned long long) * 16 * ((n + MS_BLOCK - 1) / MS_BLOCK), h->stream);
+  (void)hipMemsetAsync(h->S.stamps, 0, sizeof(unsigned long long) * MS_NSTAMP * ((n + MS_BLOCK - 1) / MS_BLOCK), h->stream);
 #endif
   if (hipMalloc((void**)&h->ctr, sizeof(Counters)) != hipSuccess) {
     (void)hipFree(h->mem);

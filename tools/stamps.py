@@ -5,7 +5,7 @@
     python tools/stamps.py [--envs N] [--steps K] [--every M]   # on the GPU box
 
 The stamps build writes s_memtime at the STAMP(k) points of ms_env.hip into a
-[wave][16] buffer. For every M-th launch of a K-step episode this tool reads the buffer
+[wave][NS] buffer. For every M-th launch of a K-step episode this tool reads the buffer
 and reports, per phase, the mean cycles over all waves and over the slowest 5 % of waves
 (the ones that set the launch time), plus the launch span in cycles.
 """
@@ -21,6 +21,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "marl-soccer_amd")
 STAMP_LIB = os.path.join(PKG, "lib", "libmarlsoccer_stamps.so")
+NS = 24  # MS_NSTAMP
+# accumulated narrowphase sub-phase cycles and iteration counts (wave max over lanes)
+ACC = {16: "AA test", 17: "AA insert", 18: "AA iterations", 19: "SA test", 20: "SA insert", 21: "SA iterations"}
 
 # (label, from, to) in kernel order; a stamp inside a branch no lane took is carried forward
 ORDER = [0, 1, 2, 11, 13, 3, 14, 4, 15, 5, 6, 7, 8, 9, 10]
@@ -45,10 +48,10 @@ def main():
     ap.add_argument("--every", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=0, help="untimed steps first (1000: steady state)")
     ap.add_argument("--out", default="")
-    a = ap.parse_args()
+    a, extra = ap.parse_known_args()
     sys.path.insert(0, PKG)
     if a.build:
-        build()
+        build(extra)
         return
     os.environ["MARL_SOCCER_LIB"] = STAMP_LIB
     import numpy as np
@@ -70,7 +73,7 @@ def main():
     acts = torch.empty((a.envs, 4, 3), device="cuda")
     seg = {k: [] for k in ORDER[1:]}
     seg_slow = {k: [] for k in ORDER[1:]}
-    spans, totals, slow_tot, maxnc = [], [], [], []
+    spans, totals, slow_tot, maxnc, worst, accs = [], [], [], [], [], []
     for t in range(a.warmup):
         acts.uniform_(-1.0, 1.0, generator=g)
         env.step(acts)
@@ -79,14 +82,14 @@ def main():
         sample = t % a.every == 0 and t > 0
         if sample:
             torch.cuda.synchronize()
-            hip.hipMemset(ptr, 0, nw * 16 * 8)
+            hip.hipMemset(ptr, 0, nw * NS * 8)
             torch.cuda.synchronize()
         env.step(acts)
         if sample:
             torch.cuda.synchronize()
-            buf = np.zeros((nw, 16), np.uint64)
+            buf = np.zeros((nw, NS), np.uint64)
             hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-            hip.hipMemcpy(buf.ctypes.data, ptr, nw * 16 * 8, 2)
+            hip.hipMemcpy(buf.ctypes.data, ptr, nw * NS * 8, 2)
             st = buf.astype(np.int64)
             maxnc.append(st[:, 12].copy())
             for i in range(1, len(ORDER)):  # carry forward stamps of untaken branches
@@ -96,7 +99,12 @@ def main():
             slow = tot >= np.quantile(tot, 0.95)
             totals.append(tot.mean())
             slow_tot.append(tot[slow].mean())
-            spans.append(st[:, 10].max() - st[:, 0].min())
+            spans.append(st[:, 10].max() - st[st[:, 0] > 0, 0].min())
+            w = int(np.argmax(tot))
+            accs.append(st[:, 16:22].copy())
+            worst.append({"cycles": int(tot[w]), "max_contacts": int(maxnc[-1][w]),
+                          "acc": {ACC[16 + j]: int(st[w, 16 + j]) for j in range(6)},
+                          "phases": {LABELS[ORDER[i]]: int(st[w, ORDER[i]] - st[w, ORDER[i - 1]]) for i in range(1, len(ORDER))}})
             for i in range(1, len(ORDER)):
                 d = st[:, ORDER[i]] - st[:, ORDER[i - 1]]
                 seg[ORDER[i]].append(d.mean())
@@ -105,6 +113,11 @@ def main():
     res = {"envs": a.envs, "steps": a.steps, "warmup": a.warmup, "samples": len(totals),
            "wave_cycles_mean": float(np.mean(totals)), "wave_cycles_slowest5pct": float(np.mean(slow_tot)),
            "launch_span_cycles": float(np.mean(spans)),
+           "worst_wave_cycles_mean": float(np.mean([w["cycles"] for w in worst])),
+           "worst_wave_max_contacts": {str(v): sum(1 for w in worst if w["max_contacts"] == v) for v in sorted({w["max_contacts"] for w in worst})},
+           "narrowphase_acc_mean": {ACC[16 + j]: round(float(np.mean(np.concatenate(accs)[:, j])), 1) for j in range(6)},
+           "worst_wave_acc_mean": {k: round(float(np.mean([w["acc"][k] for w in worst])), 1) for k in ACC.values()},
+           "worst_wave_phases_mean": {k: round(float(np.mean([w["phases"][k] for w in worst])), 1) for k in worst[0]["phases"]},
            "max_contacts_per_wave": {str(int(v)): int((mnc == v).sum()) for v in np.unique(mnc)},
            "phases": {LABELS[k]: {"mean": round(float(np.mean(seg[k])), 1),
                                   "slow5": round(float(np.mean(seg_slow[k])), 1)} for k in ORDER[1:]}}
