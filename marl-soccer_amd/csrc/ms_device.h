@@ -554,12 +554,9 @@ __device__ __forceinline__ void spawn_positions(Rng& g, int mode, float px[5], f
 // ------------------------------------------------------------------------------------------
 // Observations: Game._get_observations (game.py:258-322) -> fp32 (soccer_env.py:131)
 // ------------------------------------------------------------------------------------------
-#ifndef MS_PK_OBS
-#define MS_PK_OBS 1
-#endif
 template <bool FAST = false>
 __device__ __forceinline__ void unit_mag(float dx, float dy, float* o) {
-  if constexpr (FAST && MS_PK_OBS) {
+  if constexpr (FAST) {
     // x and y as one packed pair: d*d, the two quotients' Newton steps (div_nr per component)
     const V2 d = v2(dx, dy);
     const V2 d2 = d * d;
@@ -571,16 +568,6 @@ __device__ __forceinline__ void unit_mag(float dx, float dy, float* o) {
     o[1] = big ? q.y : 0.0f;
     mag = big ? mag : 0.0f;
     o[2] = div_nr_nonneg(mag, 1000.0f, rcp_nr(1000.0f));  // mag >= +0
-    return;
-  }
-  if constexpr (FAST) {
-    float mag = sqrt_nr(dx * dx + dy * dy);
-    const float r = rcp_nr(mag);
-    const bool big = mag > 1e-8f;
-    o[0] = big ? div_nr(dx, mag, r) : 0.0f;
-    o[1] = big ? div_nr(dy, mag, r) : 0.0f;
-    mag = big ? mag : 0.0f;
-    o[2] = div_nr(mag, 1000.0f, rcp_nr(1000.0f));
     return;
   }
   float mag = sqrtf(dx * dx + dy * dy);

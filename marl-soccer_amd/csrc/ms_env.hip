@@ -194,15 +194,8 @@ __device__ __forceinline__ void store_rng(At a, Env& E) {
 // pairs) whatever body/box each lane selects, so dynamic per-lane indexing is conflict free.
 // x/y pairs are stored together so that they load into register pairs for packed math.
 enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
-#ifndef MS_EARLY_OBS
-#define MS_EARLY_OBS 0  // 1: frames t-2, t-1 and the history slot stored before the physics
-#endif
 
-#ifndef MS_KC
-#define MS_KC 8
-#endif
-constexpr int KC = MS_KC;   // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (never seen)
-constexpr int KC0 = 4;  // entries loaded by every wave; KC0..KC-1 only by waves where some lane has them
+constexpr int KC = 4;  // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (pile-ups)
 
 struct Lds {
   Seg seg[8];  // static segments (walls, goal lines), read with per-lane indices
@@ -412,23 +405,6 @@ __device__ __forceinline__ void emit_three(const Params& P, const Snap& s2, cons
   }
 }
 
-// Frames t-2 and t-1 of every agent (MS_EARLY_OBS: stored before the physics).
-__device__ __forceinline__ void emit_two(const Params& P, const Snap& s2, const Snap& s1, float* __restrict__ row0) {
-  if (frame_inputs_in_range(P, s2) && frame_inputs_in_range(P, s1)) {
-    float a2[6][3], a1[6][3];
-    pair_vectors<true>(s2, a2);
-    pair_vectors<true>(s1, a1);
-    static_for<0, 4>([&](auto ac) __attribute__((always_inline)) {
-      constexpr int A = decltype(ac)::value;
-      agent_frame_store<true, A, 0>(P, s2, a2, row0);
-      agent_frame_store<true, A, 1>(P, s1, a1, row0);
-    });
-  } else {
-    emit_snapshot<0>(P, s2, row0);
-    emit_snapshot<1>(P, s1, row0);
-  }
-}
-
 // Frames of a reset (soccer_env.py:90-96): all three stacked frames are the current one, and
 // the history slot (t-2 for the next step) is the current snapshot too.
 __device__ __forceinline__ void snap_to_lds(float4 (*dst)[MS_BLOCK], int lane, const Snap& s) {
@@ -524,9 +500,7 @@ struct CSlot {
 #define CS_POS(m) ((int)(((m) >> 18) & 63u))
 #define CS_PAIR(m) ((int)(((m) >> 24) & 63u))
 
-#ifndef KREG
-#define KREG 8  // contacts held in registers; further ones go to the global spill (pile-ups)
-#endif
+constexpr int KREG = 8;  // contacts held in registers; further ones go to the global spill (pile-ups)
 #define MAXC (2 * MAXA)                 // contact capacity (2 per arbiter)
 
 __device__ __forceinline__ void cache_write(At a, int par, int k, uint32_t hdr, float4 j) {
@@ -671,7 +645,7 @@ __device__ __forceinline__ void lds_box(const Lds& L, int i, int lane, Box& b) {
 // impulses are read only for an entry that is aged or matched.
 struct CacheWalk {
   int par, nc_old, cur, out;
-  uint32_t pk[2];  // key bytes (pair | idle << 6) of entries 0..7
+  uint32_t pk;  // key bytes (pair | idle << 6) of entries 0..KC-1
 };
 __device__ __forceinline__ uint32_t cache_key(uint32_t hdr) { return (hdr & 63u) | (((hdr >> 8) & 3u) << 6); }
 
@@ -690,7 +664,7 @@ __device__ __forceinline__ float4 old_imp(At a, const Lds& L, int par, int k) {
 
 // key byte of the entry under the cursor (cur < nc_old)
 __device__ __forceinline__ uint32_t cur_key(At a, const CacheWalk& W) {
-  if (W.cur < KC) return ((W.cur < 4 ? W.pk[0] : W.pk[1]) >> (8 * (W.cur & 3))) & 0xffu;
+  if (W.cur < KC) return (W.pk >> (8 * W.cur)) & 0xffu;
   return cache_key(__builtin_nontemporal_load((gu32_t*)plane<uint32_t>(a, OFF_CH, W.par * MAXA + W.cur)));
 }
 // pair id under the cursor, 64 past the end of the old cache
@@ -785,7 +759,7 @@ __device__ __forceinline__ void write_arbiter_cache(At a, int npar, const CSlot&
 
 __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e, const Params& P, Env& E, float fx[4],
                                              float fy[4], float tq[4], Lds& L, unsigned long long* overflow_acc,
-                                             Snap& h2, uint32_t pk0, uint32_t pk1) {
+                                             Snap& h2, uint32_t pk0) {
   const int lane = a.lane;
   const float dt = P.dt;
   // cpBodyUpdatePosition
@@ -851,8 +825,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
   W.nc_old = META_NC(E.meta);
   W.cur = 0;
   W.out = 0;
-  W.pk[0] = pk0;
-  W.pk[1] = pk1;
+  W.pk = pk0;
 
   ACC_DECL(aa_col); ACC_DECL(aa_add); ACC_DECL(sa_col); ACC_DECL(sa_add);
 #ifdef MS_STAMPS
@@ -950,7 +923,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
   }
 
   STAMP(4);
-  if (!MS_EARLY_OBS) snap_load(a, h2);  // arrives during the solver
+  snap_load(a, h2);  // arrives during the solver
   if (C.nc > 0) {
     // cpArbiterApplyCachedImpulse, then cpArbiterApplyImpulse x 10 (pymunk Space default)
     FOR_CONTACTS(C, ovf, warm_one(P, c_, L, lane));
@@ -1060,7 +1033,6 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   load_scalars(at, E);
   load_bodies(at, E);
   Snap h2;  // obs-history snapshot t-2
-  if (MS_EARLY_OBS) snap_load(at, h2);
   float a[12];
   {
     const float4* ap = (const float4*)(actions + (active ? e : S.n - 1) * 12);
@@ -1072,43 +1044,24 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   }
   const int nco = META_NC(E.meta);
   const int par0 = (E.meta & META_PAR) ? 1 : 0;
-  // old arbiter cache entries k < KC0. No branch (so the compiler's wait counts stay exact): a
+  // old arbiter cache entries k < KC. No branch (so the compiler's wait counts stay exact): a
   // lane without entry k re-reads its own scalars/bodies, which are in L1, instead.
-  uint32_t pch[KC0];
-  float4 pcj[KC0];
+  uint32_t pch[KC];
+  float4 pcj[KC];
 #pragma unroll
-  for (int k = 0; k < KC0; ++k) {
+  for (int k = 0; k < KC; ++k) {
     const bool need = k < nco;
     const uint32_t* hp = need ? plane<uint32_t>(at, OFF_CH, par0 * MAXA + k) : (const uint32_t*)plane<int4>(at, OFF_I4, 0);
     const float4* jp = need ? plane<float4>(at, OFF_CJ, par0 * MAXA + k) : plane<float4>(at, OFF_B4, 0);
     pch[k] = *hp;
     pcj[k] = *jp;
   }
-  uint32_t pk0 = 0u, pk1 = 0u;
+  uint32_t pk0 = 0u;
 #pragma unroll
-  for (int k = 0; k < KC0; ++k) {
+  for (int k = 0; k < KC; ++k) {
     L.ch[k][lane] = pch[k];
     L.cj[k][lane] = pcj[k];
     pk0 |= cache_key(pch[k]) << (8 * k);
-  }
-  // entries KC0..KC-1 (pile-ups: a few % of the waves) under a wave-uniform branch
-  if (KC > KC0 && __ballot(nco > KC0) != 0ull) {
-    uint32_t qch[KC > KC0 ? KC - KC0 : 1];
-    float4 qcj[KC > KC0 ? KC - KC0 : 1];
-#pragma unroll
-    for (int k = KC0; k < KC; ++k) {
-      const bool need = k < nco;
-      const uint32_t* hp = need ? plane<uint32_t>(at, OFF_CH, par0 * MAXA + k) : (const uint32_t*)plane<int4>(at, OFF_I4, 0);
-      const float4* jp = need ? plane<float4>(at, OFF_CJ, par0 * MAXA + k) : plane<float4>(at, OFF_B4, 0);
-      qch[k - KC0] = *hp;
-      qcj[k - KC0] = *jp;
-    }
-#pragma unroll
-    for (int k = KC0; k < KC; ++k) {
-      L.ch[k][lane] = qch[k - KC0];
-      L.cj[k][lane] = qcj[k - KC0];
-      pk1 |= cache_key(qch[k - KC0]) << (8 * (k - KC0));
-    }
   }
 
   stage_segments(P, L, lane);
@@ -1138,25 +1091,7 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     // the end of this step
     fill3 = (E.meta & META_HE) != 0 || (P.autoreset && done_now);
     snap_of(E, h1);
-#if MS_EARLY_OBS
-    // frames t-2 and t-1 and the history slot do not depend on this step's physics: stored now,
-    // while the physics runs (a refilled stack writes three copies of frame t at the end instead)
-    if (!fill3) {
-      if (obs) emit_two(P, h2, h1, obs + e * 264);
-      snap_store(at, h1);  // t-1 becomes the next step's t-2
-    }
-    {
-      // step-start positions (the reward's previous state) staged in LDS across the physics
-      float f[12];
-#pragma unroll
-      for (int b = 0; b < 5; ++b) { f[b] = h1.px[b]; f[5 + b] = h1.py[b]; }
-      f[10] = 0.0f; f[11] = 0.0f;
-#pragma unroll
-      for (int g = 0; g < 3; ++g) L.h1[g][lane] = make_float4(f[4 * g], f[4 * g + 1], f[4 * g + 2], f[4 * g + 3]);
-    }
-#else
     snap_to_lds(L.h1, lane, h1);  // back at the end: not held in registers across the physics
-#endif
   }
 
   float pvx[5], pvy[5];
@@ -1182,29 +1117,16 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
 
     unsigned long long ovf = 0;
     STAMP(1);
-    physics_step(S, at, e, P, E, fx, fy, tq, L, &ovf, h2, pk0, pk1);
+    physics_step(S, at, e, P, E, fx, fy, tq, L, &ovf, h2, pk0);
     // positions back from LDS (written by the position phase, unchanged since)
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
       const V2 p = L.ph.p[b][lane];
       E.px[b] = p.x; E.py[b] = p.y;
     }
-#if MS_EARLY_OBS
-    {
-      float f[12];
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        const float4 v = L.h1[g][lane];
-        f[4 * g] = v.x; f[4 * g + 1] = v.y; f[4 * g + 2] = v.z; f[4 * g + 3] = v.w;
-      }
-#pragma unroll
-      for (int b = 0; b < 5; ++b) { pvx[b] = f[b]; pvy[b] = f[5 + b]; }
-    }
-#else
     snap_from_lds(L.h1, lane, h1);
 #pragma unroll
     for (int b = 0; b < 5; ++b) { pvx[b] = h1.px[b]; pvy[b] = h1.py[b]; }
-#endif
     STAMP(7);
     if (ovf) atomicAdd(&ctr->overflow, ovf);
 
@@ -1242,8 +1164,6 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     if (fill3) {
       emit_fill3(at, P, e, s0, obs);
       E.meta &= ~META_HE;
-    } else if (MS_EARLY_OBS) {
-      if (obs) emit_snapshot<2>(P, s0, obs + e * 264);  // frame t; t-2, t-1 went out before the physics
     } else {
       if (obs) emit_three(P, h2, h1, s0, obs + e * 264);
       snap_store(at, h1);  // t-1 becomes the next step's t-2
