@@ -193,7 +193,6 @@ __device__ __forceinline__ void store_rng(At a, Env& E) {
 // Layouts are [field][index][lane]: the 64 lanes of a wave hit 64 distinct dwords (or 8-byte
 // pairs) whatever body/box each lane selects, so dynamic per-lane indexing is conflict free.
 // x/y pairs are stored together so that they load into register pairs for packed math.
-enum { BX_PX = 0, BX_PY, BX_C, BX_S, BX_N };
 
 constexpr int KC = 4;  // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (pile-ups)
 
@@ -203,7 +202,7 @@ struct Lds {
     V2 p[6][MS_BLOCK];             // body position (body 5 = static, all 0)
     float4 vw[6][MS_BLOCK];        // velocity x, y, angular velocity (one 12-B access per body)
     float4 bw[6][MS_BLOCK];        // bias velocity x, y, bias angular velocity
-    float box[BX_N][4][MS_BLOCK];  // agent box transform (p, cos, sin)
+    float4 box[4][MS_BLOCK];  // agent box transform (px, py, cos, sin): one 16-B read per box
   } ph;
   // previous step's arbiter cache, entries 0..KC-1 (loaded with the state at kernel start)
   uint32_t ch[KC][MS_BLOCK];
@@ -212,8 +211,12 @@ struct Lds {
 };
 
 // body velocity (v, w) and bias velocity (vb, wb) of body b in LDS
+// full 16-B reads (ds_read_b128: 4 LDS cycles per wave-instruction; the 12-B ds_read_b96 the
+// compiler narrows a 3-float use to takes 8)
+typedef float F4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ F4 lds_f4(const float4* p) { return __builtin_nontemporal_load((const F4*)p); }
 __device__ __forceinline__ void ld_v(const Lds& L, int b, int lane, V2& v, float& w) {
-  const float4 q = L.ph.vw[b][lane];
+  const F4 q = lds_f4(&L.ph.vw[b][lane]);
   v = v2(q.x, q.y); w = q.z;
 }
 __device__ __forceinline__ void st_v(Lds& L, int b, int lane, V2 v, float w) {
@@ -221,7 +224,7 @@ __device__ __forceinline__ void st_v(Lds& L, int b, int lane, V2 v, float w) {
   d[0] = v.x; d[1] = v.y; d[2] = w;
 }
 __device__ __forceinline__ void ld_vb(const Lds& L, int b, int lane, V2& v, float& w) {
-  const float4 q = L.ph.bw[b][lane];
+  const F4 q = lds_f4(&L.ph.bw[b][lane]);
   v = v2(q.x, q.y); w = q.z;
 }
 __device__ __forceinline__ void st_vb(Lds& L, int b, int lane, V2 v, float w) {
@@ -634,7 +637,8 @@ __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int
 }
 
 __device__ __forceinline__ void lds_box(const Lds& L, int i, int lane, Box& b) {
-  box_world(L.ph.box[BX_PX][i][lane], L.ph.box[BX_PY][i][lane], L.ph.box[BX_C][i][lane], L.ph.box[BX_S][i][lane], b);
+  const F4 t = lds_f4(&L.ph.box[i][lane]);
+  box_world(t.x, t.y, t.z, t.w, b);
 }
 
 // Old-cache cursor: the previous step's arbiter cache (sorted by pair id) is streamed once,
@@ -780,8 +784,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     box_world(E.px[b], E.py[b], c, s, bx);
 #pragma unroll
     for (int q = 0; q < 4; ++q) bb_[b][q] = bx.bb[q];
-    L.ph.box[BX_PX][b][lane] = E.px[b]; L.ph.box[BX_PY][b][lane] = E.py[b];
-    L.ph.box[BX_C][b][lane] = c; L.ph.box[BX_S][b][lane] = s;
+    L.ph.box[b][lane] = make_float4(E.px[b], E.py[b], c, s);
   }
 #pragma unroll
   for (int b = 0; b < 5; ++b) {
