@@ -290,19 +290,23 @@ def test_actions_out_of_range_are_clipped(ms):
 
 # ---- full-size properties (BASELINE configs) ------------------------------------------------
 
-@pytest.mark.parametrize("n,max_steps,steps", [(4096, 50, 120), (32768, 512, 560), (65536, 50, 120)])
-def test_full_size_subsample_and_invariants(ms, n, max_steps, steps):
-    """BASELINE config sizes: 4,096 and 65,536 envs per GPU (configs 2-4) and one GPU's shard of
-    config 5 (262,144 envs / 8 GPUs = 32,768, max_steps=512, default reward shaping, a whole
-    episode plus its auto-reset). The 64-env subsample matches the fp32 oracle bit for bit,
-    state stays finite and inside the field, results are independent of the batch they run in."""
+@pytest.mark.parametrize("n,max_steps,steps,env0", [(4096, 50, 120, 0), (8192, 1000, 120, 3 * 8192),
+                                                    (32768, 512, 560, 5 * 32768), (65536, 50, 120, 0)])
+def test_full_size_subsample_and_invariants(ms, n, max_steps, steps, env0):
+    """BASELINE config sizes: 4,096 and 65,536 envs per GPU (configs 1-2), rank 3's shard of
+    config 4 (65,536 envs / 8 GPUs = 8,192, global envs 24,576..32,767) and rank 5's shard of
+    config 5 (262,144 / 8 = 32,768, max_steps=512, default reward shaping, a whole episode plus
+    its auto-reset). A shard is seeded and driven by its global env indices (seed 19 + g, actions
+    a function of g), as bench.py and marlsoccer.distributed do. The 64-env subsample matches the
+    fp32 oracle bit for bit, state stays finite and inside the field, results are independent of
+    the batch they run in."""
     gpu = ms.SoccerBatch(n, config=cfg_dict(max_steps=max_steps))
-    gpu.reset(seed=19)
+    gpu.reset(seed=19 + env0)
     sub = np.linspace(0, n - 1, 64).astype(np.int64)
     ref = orc.OracleBatch(64, "f32", oracle_cfg(gpu._cfg))
-    ref.reset(np.stack([orc.pcg_from_seed(19 + int(i)) for i in sub]), 0)
+    ref.reset(np.stack([orc.pcg_from_seed(19 + env0 + int(i)) for i in sub]), 0)
     for t in range(steps):
-        act = sh.hash_actions(n, t)
+        act = sh.hash_actions(n, t, env0=env0)
         out = gpu.step(torch.from_numpy(act).to(gpu.device))
         robs = ref.step(act[sub])[0]
         if t % 20 == 19:
