@@ -15,6 +15,9 @@
  *                               -> Game.step (game/game.py:378-437)
  *                               -> pymunk.Space.step(1/60) -> cpSpaceStep (Chipmunk2D, cffi)
  *                                  with the entities.py:19-28 / :69-77 velocity callbacks
+ *   ms_step_ring /           <- the same step / reset with the stacked observation kept as a
+ *   ms_reset_ring               window into a per-agent frame ring (opt-in; the frame-stack
+ *                               deque of soccer_env.py:130-140 without re-writing old frames)
  *   ms_observe               <- Game._get_observations (game/game.py:258-322)
  *   ms_seed_pcg64            <- np.random.default_rng(seed) (game/game.py:81-85): numpy
  *                               SeedSequence -> PCG64 state, restated so a C caller can seed
@@ -213,6 +216,23 @@ int ms_reset(ms_env *env, const uint64_t *pcg, const uint8_t *env_mask, int mode
  * ms_stats (read with ms_get_stats, which synchronises). */
 int ms_step(ms_env *env, const float *actions, float *obs, float *rew, uint8_t *term,
             uint8_t *trunc, int8_t *goal, int32_t *score);
+
+/* Frame-ring observations (opt-in; replaces the deque of 3 frames of soccer_env.py:130-140
+ * and marl_vecenv.py:30-68 with a window into a longer per-agent ring, so a step writes one
+ * frame instead of three). `frames`: device float [N][4][R][22], 16-B aligned, R even >= 4.
+ * The step's stacked observation of env e, agent a is frames[e][a][pos .. pos+2] (t-2, t-1,
+ * t): 66 contiguous floats, row stride R*22. ms_step_ring writes frame t at pos+2; with
+ * wrap = 1 it also writes t-2 and t-1 at pos, pos+1 (use when the window moves back to the
+ * start of the ring); with wrap = 0 the caller guarantees slots pos, pos+1 hold the previous
+ * two steps' frames t (window advanced by one). Envs that are reset (auto-reset, or the
+ * first step after ms_create) get 3 copies of the reset frame, as ms_step. Otherwise as
+ * ms_step (obs replaced by the ring). 0 <= pos <= R-3, else MS_ERR_INVALID_ARGUMENT. */
+int ms_step_ring(ms_env *env, const float *actions, float *frames, int R, int pos, int wrap,
+                 float *rew, uint8_t *term, uint8_t *trunc, int8_t *goal, int32_t *score);
+
+/* ms_reset writing the 3 stacked copies of the reset frame into ring slots pos..pos+2. */
+int ms_reset_ring(ms_env *env, const uint64_t *pcg, const uint8_t *env_mask, int mode,
+                  float *frames, int R, int pos);
 
 /* Current frame of every agent (Game._get_observations), device float [N][4][22]. */
 int ms_observe(ms_env *env, float *frames);

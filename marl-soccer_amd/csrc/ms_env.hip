@@ -444,6 +444,120 @@ __device__ __forceinline__ void emit_fill3(At a, const Params& P, int64_t e, con
   snap_store(a, s0);
 }
 
+// ---- frame-ring observations (ms_step_ring) -------------------------------------------------
+// The stacked observation as a window of three consecutive frames of a per-env, per-agent ring
+// of R 22-float frames: row [env][agent] holds R frames, the step's obs is frames pos..pos+2
+// (t-2, t-1, t), which the caller views as an (N, 4, 66) tensor with a row stride of R*22
+// floats. A step writes frame t only (at pos+2); frames t-2 and t-1 are the previous steps'
+// frames t, already in place. When the window wraps to the start of the ring (pos = 0) the step
+// writes all three (t-2 and t-1 from their snapshots), and a refilled stack (reset, auto-reset)
+// writes frame t three times, as the contiguous layout does.
+struct Ring {
+  float* frames;
+  int R;     // frames per ring row (even: every frame slot of an even index is 16-B aligned)
+  int pos;   // ring slot of frame t-2 in this step's window
+  int wrap;  // 1: frames t-2, t-1 are written too
+};
+
+// agent_frame_store with the destination and its 16-B alignment (`al`) as runtime values. The
+// arithmetic is agent_frame_store's, restated rather than shared on purpose: factoring the two
+// through one helper changes the register allocation of ms_step_kernel (its ISA is otherwise
+// instruction-for-instruction what it was before the ring existed; checked with --cuda-device-only -S).
+template <bool FAST, int A>
+__device__ __forceinline__ void frame_store_at(const Params& P, const Snap& s, const float aa[6][3],
+                                               float* __restrict__ d, bool al) {
+  // obs slots 4 (teammate), 7, 10 (opponents in index order) -> (pair, mirrored)
+  constexpr int TEAM = A ^ 1, O1 = A < 2 ? 2 : 0, O2 = A < 2 ? 3 : 1;
+  constexpr int OTH[3] = {TEAM, O1, O2};
+  float f[22];
+  if constexpr (FAST) {
+    f[0] = div_nr(s.vx[A], P.obs_vmax, rcp_nr(P.obs_vmax));
+    f[1] = div_nr(s.vy[A], P.obs_vmax, rcp_nr(P.obs_vmax));
+    f[3] = div_nr(s.w[A], P.obs_wmax, rcp_nr(P.obs_wmax));
+  } else {
+    f[0] = s.vx[A] / P.obs_vmax;
+    f[1] = s.vy[A] / P.obs_vmax;
+    f[3] = s.w[A] / P.obs_wmax;
+  }
+  f[2] = angle_obs<FAST>(s.ang[A]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int B = OTH[k];
+    const int lo = A < B ? A : B, hi = A < B ? B : A;
+    const int p = lo == 0 ? hi - 1 : (lo == 1 ? hi + 1 : 5);
+    if (A < B) {
+      f[4 + 3 * k] = aa[p][0]; f[5 + 3 * k] = aa[p][1];
+    } else {
+      f[4 + 3 * k] = 0.0f - aa[p][0]; f[5 + 3 * k] = 0.0f - aa[p][1];
+    }
+    f[6 + 3 * k] = aa[p][2];
+  }
+  unit_mag<FAST>(s.px[4] - s.px[A], s.py[4] - s.py[A], f + 13);
+  const float own_x = A < 2 ? 10.0f : 790.0f, opp_x = A < 2 ? 790.0f : 10.0f;
+  unit_mag<FAST>(own_x - s.px[A], 300.0f - s.py[A], f + 16);
+  unit_mag<FAST>(opp_x - s.px[A], 300.0f - s.py[A], f + 19);
+  if (al) {  // 16-B aligned: five 16-B stores and one 8-B store
+#pragma unroll
+    for (int q = 0; q < 5; ++q) obs_put((float4*)(d + 4 * q), make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]));
+    obs_put((float2*)(d + 20), make_float2(f[20], f[21]));
+  } else {  // starts half-way into a 16-B word: the 8-B store first
+    obs_put((float2*)d, make_float2(f[0], f[1]));
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+      obs_put((float4*)(d + 2 + 4 * q), make_float4(f[2 + 4 * q], f[3 + 4 * q], f[4 + 4 * q], f[5 + 4 * q]));
+  }
+}
+
+// The four agents' frames of snapshot s at ring slot `slot` of the env's rows; AL: slot is even
+// (16-B aligned). The alignment is a template argument so every frame is stored as 16-B and 8-B
+// vector stores: with a runtime alignment the two store sequences are merged at 4-B alignment
+// and split into single dwords.
+template <bool AL>
+__device__ __forceinline__ void ring_emit(const Params& P, const Snap& s, float* __restrict__ row, int R, int slot) {
+  float* d0 = row + slot * 22;
+  if (frame_inputs_in_range(P, s)) {
+    float aa[6][3];
+    pair_vectors<true>(s, aa);
+    static_for<0, 4>([&](auto ac) __attribute__((always_inline)) {
+      constexpr int A = decltype(ac)::value;
+      frame_store_at<true, A>(P, s, aa, d0 + A * R * 22, AL);
+    });
+  } else {
+    float aa[6][3];
+    pair_vectors<false>(s, aa);
+    static_for<0, 4>([&](auto ac) __attribute__((always_inline)) {
+      constexpr int A = decltype(ac)::value;
+      frame_store_at<false, A>(P, s, aa, d0 + A * R * 22, AL);
+    });
+  }
+}
+
+__device__ __forceinline__ void snap_select(bool c, const Snap& a, const Snap& b, Snap& o) {
+#pragma unroll
+  for (int q = 0; q < 5; ++q) { o.px[q] = c ? a.px[q] : b.px[q]; o.py[q] = c ? a.py[q] : b.py[q]; }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    o.vx[q] = c ? a.vx[q] : b.vx[q]; o.vy[q] = c ? a.vy[q] : b.vy[q];
+    o.ang[q] = c ? a.ang[q] : b.ang[q]; o.w[q] = c ? a.w[q] : b.w[q];
+  }
+}
+
+// The frames a step writes into its window pos..pos+2: frame t (s0) at pos+2 always; with
+// `refill` (reset, auto-reset) s0 at pos and pos+1 too, else on a wrap t-2 (h2) and t-1 (h1).
+// One loop over the slots keeps a single copy of the frame code per alignment.
+__device__ __forceinline__ void ring_emit_window(const Params& P, const Snap& h2, const Snap& h1, const Snap& s0,
+                                                 bool refill, float* __restrict__ row, const Ring& rg) {
+  const int k0 = (refill || rg.wrap) ? 0 : 2;
+#pragma unroll 1
+  for (int k = k0; k < 3; ++k) {
+    Snap s;
+    snap_select(k == 2 || refill, s0, k == 0 ? h2 : h1, s);
+    const int slot = rg.pos + k;
+    if (slot & 1) ring_emit<false>(P, s, row, rg.R, slot);
+    else ring_emit<true>(P, s, row, rg.R, slot);
+  }
+}
+
 // Game.reset (game.py:76-118): fresh bodies, score/steps 0, arbiters dropped, spawn.
 __device__ __forceinline__ void reset_env_regs(Env& E, int mode) {
 #pragma unroll
@@ -763,7 +877,7 @@ __device__ __forceinline__ void write_arbiter_cache(At a, int npar, const CSlot&
 
 __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e, const Params& P, Env& E, float fx[4],
                                              float fy[4], float tq[4], Lds& L, unsigned long long* overflow_acc,
-                                             Snap& h2, uint32_t pk0) {
+                                             Snap& h2, uint32_t pk0, bool need_h2) {
   const int lane = a.lane;
   const float dt = P.dt;
   // cpBodyUpdatePosition
@@ -926,7 +1040,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
   }
 
   STAMP(4);
-  snap_load(a, h2);  // arrives during the solver
+  if (need_h2) snap_load(a, h2);  // arrives during the solver
   if (C.nc > 0) {
     // cpArbiterApplyCachedImpulse, then cpArbiterApplyImpulse x 10 (pymunk Space default)
     FOR_CONTACTS(C, ovf, warm_one(P, c_, L, lane));
@@ -1016,11 +1130,12 @@ __host__ __device__ constexpr Params default_params() {
      {10.0f, 225.0f, 10.0f, 375.0f, -1.0f, 0.0f, 1.0f, {9.0f, 224.0f, 11.0f, 376.0f}},
      {790.0f, 225.0f, 790.0f, 375.0f, -1.0f, 0.0f, 1.0f, {789.0f, 224.0f, 791.0f, 376.0f}}}};
 }
+template <bool RING>
 __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, const float* __restrict__ actions,
                                           float* __restrict__ obs, float* __restrict__ rew,
                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
                                           int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
-                                          Counters* ctr) {
+                                          Counters* ctr, const Ring rg) {
   __shared__ Lds L;
   STAMP(0);
   const int lane = threadIdx.x;
@@ -1120,7 +1235,7 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
 
     unsigned long long ovf = 0;
     STAMP(1);
-    physics_step(S, at, e, P, E, fx, fy, tq, L, &ovf, h2, pk0);
+    physics_step(S, at, e, P, E, fx, fy, tq, L, &ovf, h2, pk0, !RING || rg.wrap != 0);
     // positions back from LDS (written by the position phase, unchanged since)
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
@@ -1164,7 +1279,15 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     // (4) frame t; refilled stacks get all three frames and the history slot
     Snap s0;
     snap_of(E, s0);
-    if (fill3) {
+    if constexpr (RING) {
+      ring_emit_window(P, h2, h1, s0, fill3, rg.frames + e * (int64_t)(4 * rg.R * 22), rg);
+      if (fill3) {
+        snap_store(at, s0);
+        E.meta &= ~META_HE;
+      } else {
+        snap_store(at, h1);  // t-1 becomes the next step's t-2
+      }
+    } else if (fill3) {
       emit_fill3(at, P, e, s0, obs);
       E.meta &= ~META_HE;
     } else {
@@ -1185,19 +1308,37 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params Pi
                                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
                                                            int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
                                                            Counters* ctr) {
+  const Ring none{nullptr, 0, 0, 0};
   if constexpr (DEFAULT_PARAMS) {
     Params Pd = default_params();
     Pd.max_steps = Pin.max_steps;  // episode length and auto-reset stay runtime values
     Pd.autoreset = Pin.autoreset;
-    step_envs(S, Pd, actions, obs, rew, term, trunc, goal_out, score_out, ctr);
+    step_envs<false>(S, Pd, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
   } else {
-    step_envs(S, Pin, actions, obs, rew, term, trunc, goal_out, score_out, ctr);
+    step_envs<false>(S, Pin, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
+  }
+}
+
+// ms_step with the observation as a frame-ring window (ms_step_ring)
+template <bool DEFAULT_PARAMS>
+__global__ __launch_bounds__(MS_BLOCK) void ms_step_ring_kernel(DevState S, Params Pin, const float* __restrict__ actions,
+                                                                Ring rg, float* __restrict__ rew,
+                                                                uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                                int8_t* __restrict__ goal_out,
+                                                                int32_t* __restrict__ score_out, Counters* ctr) {
+  if constexpr (DEFAULT_PARAMS) {
+    Params Pd = default_params();
+    Pd.max_steps = Pin.max_steps;
+    Pd.autoreset = Pin.autoreset;
+    step_envs<true>(S, Pd, actions, nullptr, rew, term, trunc, goal_out, score_out, ctr, rg);
+  } else {
+    step_envs<true>(S, Pin, actions, nullptr, rew, term, trunc, goal_out, score_out, ctr, rg);
   }
 }
 
 __global__ __launch_bounds__(MS_BLOCK) void ms_reset_kernel(DevState S, Params P, const uint64_t* __restrict__ pcg,
                                                             const uint8_t* __restrict__ mask, int mode, int set_hist_empty,
-                                                            float* __restrict__ obs) {
+                                                            float* __restrict__ obs, const Ring rg) {
   const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + threadIdx.x;
   const bool active = e < S.n && (!mask || mask[e]);
   if (!active) return;
@@ -1215,6 +1356,9 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_reset_kernel(DevState S, Params P
   Snap s0;
   snap_of(E, s0);
   emit_fill3(a, P, e, s0, obs);
+  if (rg.frames) {
+    ring_emit_window(P, s0, s0, s0, true, rg.frames + e * (int64_t)(4 * rg.R * 22), rg);
+  }
   E.meta &= ~META_HE;
   if (set_hist_empty) E.meta |= META_HE;
   store_rng(a, E);
@@ -1580,7 +1724,8 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
   }
   HIPCHK(hipMemcpyAsync(dp, hp, sizeof(uint64_t) * 4 * n, hipMemcpyHostToDevice, h->stream));
   hipLaunchKernelGGL(ms_reset_kernel, dim3(grid_for(n_envs, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S, h->P,
-                     (const uint64_t*)dp, (const uint8_t*)nullptr, (int)MS_SPAWN_RANDOM, 1, (float*)nullptr);
+                     (const uint64_t*)dp, (const uint8_t*)nullptr, (int)MS_SPAWN_RANDOM, 1, (float*)nullptr,
+                     Ring{nullptr, 0, 0, 0});
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(h->stream));
   (void)hipFree(dp);
@@ -1612,7 +1757,7 @@ int ms_reset(ms_env* h, const uint64_t* pcg, const uint8_t* mask, int mode, floa
   if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_reset: null handle");
   if (mode < 0 || mode > 2) return fail(MS_ERR_INVALID_ARGUMENT, "ms_reset: mode must be 0, 1 or 2");
   hipLaunchKernelGGL(ms_reset_kernel, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S, h->P, pcg,
-                     mask, mode, 0, obs);
+                     mask, mode, 0, obs, Ring{nullptr, 0, 0, 0});
   HIPCHK(hipGetLastError());
   return MS_OK;
 }
@@ -1630,6 +1775,46 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
   else
     hipLaunchKernelGGL(ms_step_kernel<false>, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S,
                        h->P, actions, obs, rew, term, trunc, goal, score, h->ctr);
+  HIPCHK(hipGetLastError());
+  return MS_OK;
+}
+
+// Frame-ring arguments: frames 16-B aligned, R even and >= 4, window pos..pos+2 inside the row.
+static int ring_check(const char* fn, const float* frames, int R, int pos, int wrap) {
+  if (!frames || ((uintptr_t)frames & 15u) || R < 4 || (R & 1) || pos < 0 || pos + 3 > R || (wrap != 0 && wrap != 1)) {
+    const std::string msg = std::string(fn) +
+                            ": bad frame ring (frames 16-B aligned, R even >= 4, 0 <= pos <= R-3, wrap 0 or 1; got R=" +
+                            std::to_string(R) + " pos=" + std::to_string(pos) + " wrap=" + std::to_string(wrap) + ")";
+    return fail(MS_ERR_INVALID_ARGUMENT, msg);
+  }
+  return MS_OK;
+}
+
+int ms_reset_ring(ms_env* h, const uint64_t* pcg, const uint8_t* mask, int mode, float* frames, int R, int pos) {
+  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_reset_ring: null handle");
+  if (mode < 0 || mode > 2) return fail(MS_ERR_INVALID_ARGUMENT, "ms_reset_ring: mode must be 0, 1 or 2");
+  if (int rc = ring_check("ms_reset_ring", frames, R, pos, 0)) return rc;
+  hipLaunchKernelGGL(ms_reset_kernel, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S, h->P, pcg,
+                     mask, mode, 0, (float*)nullptr, Ring{frames, R, pos, 0});
+  HIPCHK(hipGetLastError());
+  return MS_OK;
+}
+
+int ms_step_ring(ms_env* h, const float* actions, float* frames, int R, int pos, int wrap, float* rew, uint8_t* term,
+                 uint8_t* trunc, int8_t* goal, int32_t* score) {
+  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_ring: null handle");
+  if (!actions) return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_ring: actions are required");
+  if (int rc = ring_check("ms_step_ring", frames, R, pos, wrap)) return rc;
+  if (((uintptr_t)actions & 15u) || ((uintptr_t)rew & 15u) || ((uintptr_t)term & 3u) || ((uintptr_t)trunc & 3u) ||
+      ((uintptr_t)score & 7u))
+    return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_ring: misaligned buffer (actions/rew 16 B, score 8 B, flags 4 B)");
+  const Ring rg{frames, R, pos, wrap};
+  if (h->default_params)
+    hipLaunchKernelGGL(ms_step_ring_kernel<true>, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S,
+                       h->P, actions, rg, rew, term, trunc, goal, score, h->ctr);
+  else
+    hipLaunchKernelGGL(ms_step_ring_kernel<false>, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S,
+                       h->P, actions, rg, rew, term, trunc, goal, score, h->ctr);
   HIPCHK(hipGetLastError());
   return MS_OK;
 }

@@ -61,7 +61,7 @@ EXPORTED = (
     "ms_config_default", "ms_create", "ms_destroy", "ms_set_stream", "ms_num_envs", "ms_seed_pcg64",
     "ms_seed_pcg64_range", "ms_reset", "ms_step", "ms_observe", "ms_export_state", "ms_import_state",
     "ms_debug_rewards", "ms_get_stats", "ms_reset_stats", "ms_last_error", "ms_abi_version",
-    "ms_config_specialised",
+    "ms_config_specialised", "ms_step_ring", "ms_reset_ring",
 )
 
 _lib = None
@@ -108,6 +108,11 @@ def lib():
     if hasattr(L, "ms_config_specialised"):  # absent only in older builds timed by tools/variants.py
         L.ms_config_specialised.argtypes = [C.POINTER(MsConfig)]
         L.ms_config_specialised.restype = C.c_int
+    if hasattr(L, "ms_step_ring"):  # likewise
+        L.ms_step_ring.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P]
+        L.ms_step_ring.restype = C.c_int
+        L.ms_reset_ring.argtypes = [P, P, P, C.c_int, P, C.c_int, C.c_int]
+        L.ms_reset_ring.restype = C.c_int
     for fn in ("ms_create", "ms_destroy", "ms_set_stream", "ms_seed_pcg64", "ms_seed_pcg64_range", "ms_reset",
                "ms_step", "ms_observe", "ms_export_state", "ms_import_state", "ms_debug_rewards",
                "ms_get_stats", "ms_reset_stats"):

@@ -329,3 +329,117 @@ class SoccerBatch:
         """Launch subsequent calls on `stream` (e.g. a graph-capture stream; ms_set_stream)."""
         N.check(self._L.ms_set_stream(self._h, C.c_void_p(stream.cuda_stream)), "ms_set_stream")
         self.stream = stream
+
+
+class FrameRingBatch(SoccerBatch):
+    """SoccerBatch whose stacked observation is a window into a per-agent ring of R frames
+    (ms_step_ring / ms_reset_ring): a step writes 352 B of obs per env instead of 1,056 B.
+
+    The step's observation is `self.obs`, an (N, 4, 66) view of `self.frames` (N, 4, R, 22)
+    with a row stride of R * 22 floats: frames pos..pos+2 = t-2, t-1, t, the same values the
+    contiguous layout holds (soccer_env.py:130-140). The view is valid until the next step or
+    reset moves the window; copy it (or index the ring with `window_index`) to keep it. Every
+    R - 2 steps the window moves back to the ring's start and that step writes all three
+    frames. An env not stepped because of a non-finite action keeps stale frames in its window
+    (SoccerBatch leaves its previous observation; both raise via raise_if_nonfinite).
+    """
+
+    def __init__(self, num_envs: int, ring: int = 32, **kw):
+        super().__init__(num_envs, **kw)
+        ring = int(ring)
+        if ring < 4 or ring % 2:
+            raise ValueError(f"ring must be even and >= 4, got {ring}")
+        if not hasattr(self._L, "ms_step_ring"):
+            raise RuntimeError("libmarlsoccer.so predates ms_step_ring; rebuild it")
+        self.ring = ring
+        self.frames = torch.zeros((self.num_envs, 4, ring, 22), dtype=torch.float32, device=self.device)
+        self._rows = self.frames.view(self.num_envs, 4, ring * 22)
+        self.pos = 0
+        self.obs = self._window(0)
+        # the packed buffer's obs region is not written by the ring kernels
+        self._ring_ptrs = None
+
+    def _window(self, pos: int) -> torch.Tensor:
+        return self._rows[:, :, 22 * pos:22 * pos + 66]
+
+    def window_index(self) -> int:
+        """Ring slot of frame t-2 of the current observation."""
+        return self.pos
+
+    def next_window(self, pos: int) -> tuple[int, int]:
+        """(pos, wrap) of the step after one whose window starts at `pos`."""
+        return (pos + 1, 0) if pos + 4 <= self.ring else (0, 1)
+
+    def reset(self, seed=None, options=None, mask: torch.Tensor | None = None, out=None):
+        """SoccerBatch.reset; the reset frame fills the current window (all envs: the window
+        moves to the ring's start)."""
+        if out is not None:
+            raise ValueError("FrameRingBatch.reset writes into the ring (out= is not supported)")
+        mode = spawn_mode(options)
+        pcg_t = None
+        if seed is not None:
+            if isinstance(seed, (int, np.integer)):
+                pcg = N.pcg_states_for_range(int(seed), self.num_envs)
+            else:
+                pcg = np.ascontiguousarray(seed, dtype=np.uint64).reshape(self.num_envs, 4)
+            pcg_t = torch.from_numpy(pcg.view(np.int64)).to(self.device)
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        else:
+            self.pos = 0
+        with torch.cuda.device(self.device):
+            cur = self._enter()
+            N.check(self._L.ms_reset_ring(self._h, self._ptr(pcg_t), self._ptr(m), mode,
+                                          C.c_void_p(self.frames.data_ptr()), self.ring, self.pos), "ms_reset_ring")
+            self._leave(cur, pcg_t, m)
+        self.obs = self._window(self.pos)
+        return self.obs
+
+    def step(self, actions: torch.Tensor, check: bool = False) -> StepOutput:
+        if actions.shape != (self.num_envs, 4, 3):
+            raise ValueError(f"actions must have shape ({self.num_envs}, 4, 3), got {tuple(actions.shape)}")
+        if actions.dtype != torch.float32:
+            actions = actions.float()
+        if actions.device != self.device:
+            raise ValueError(f"tensor on {actions.device}, env on {self.device}")
+        actions = actions.contiguous()
+        if self._ring_ptrs is None:
+            self._ring_ptrs = tuple(self._ptr(t) for t in (self.rew, self.term, self.trunc, self.goal, self.score))
+        pos, wrap = self.next_window(self.pos)
+        with torch.cuda.device(self.device):
+            cur = self._enter()
+            rc = self._L.ms_step_ring(self._h, C.c_void_p(actions.data_ptr()), C.c_void_p(self.frames.data_ptr()),
+                                      self.ring, pos, wrap, *self._ring_ptrs)
+            self._leave(cur, actions)
+        if rc:
+            N.check(rc, "ms_step_ring")
+        self.pos = pos
+        self.obs = self._window(pos)
+        if check:
+            self.raise_if_nonfinite(actions)
+        return StepOutput((self.obs, self.rew, self.term, self.trunc, self.goal, self.score))
+
+    def step_into(self, *a, **kw):
+        raise NotImplementedError("FrameRingBatch writes observations into its ring; use step()")
+
+    def launcher(self, actions: list, rew=None, term=None, trunc=None, goal=None, score=None):
+        """Pre-bound ms_step_ring for a hot loop (SoccerBatch.launcher without obs): f(i)
+        steps with actions[i % len] and advances the window."""
+        if torch.cuda.current_device() != self.device.index:
+            raise RuntimeError("launcher(): make the env's device current (torch.cuda.set_device)")
+        fn, h, R, fr = self._L.ms_step_ring, self._h, self.ring, C.c_void_p(self.frames.data_ptr())
+        outs = tuple(self._ptr(t) for t in (rew, term, trunc, goal, score))
+        acts = [self._ptr(a.contiguous()) for a in actions]
+        keep = (actions, rew, term, trunc, goal, score)
+        n = len(acts)
+
+        def step(i: int) -> None:
+            pos, wrap = self.next_window(self.pos)
+            rc = fn(h, acts[i % n], fr, R, pos, wrap, *outs)
+            if rc:
+                N.check(rc, "ms_step_ring")
+            self.pos = pos
+
+        step._keepalive = keep
+        return step
