@@ -41,6 +41,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # moves (the t-2 history as a 104-B snapshot instead of two 352-B frames, RNG
 # only on respawns) are reported beside it as layout_bytes_per_env_step.
 SURVEY_BYTES = 2289
+# The frame-ring variant (--frame-ring R) needs neither the prior frames' 704-B read nor their
+# 704-B re-write: 881 + 2C, plus the two frames a wrap re-writes every R - 2 steps.
+RING_BYTES = SURVEY_BYTES - 704 - 704
 ARB_BYTES = 20
 LAYOUT_READ = 48 + 176 + 16 + 104
 LAYOUT_WRITE = 176 + 16 + 104 + 1056 + 16 + 4 + 4 + 1 + 8  # bodies, scalars, snapshot, obs, rew, term, trunc, goal, score
@@ -58,6 +61,9 @@ def parse():
                     help="distinct device action buffers cycled (0: one per step, capped at --action-gib)")
     ap.add_argument("--action-gib", type=float, default=8.0, help="HBM cap for the action pool")
     ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of obs after every step")
+    ap.add_argument("--frame-ring", type=int, default=0, metavar="R",
+                    help="opt-in frame-ring observations (FrameRingBatch, R frames per agent ring); "
+                         "default 0: the reference's contiguous (N, 4, 66) stacked obs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-envs", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -162,7 +168,7 @@ def main():
     dev = torch.device("cuda", ordinal if world > 1 else 0)
     torch.cuda.set_device(dev)
 
-    from marlsoccer import SoccerBatch
+    from marlsoccer import FrameRingBatch, SoccerBatch
 
     E = args.envs
     cfg = None
@@ -170,7 +176,11 @@ def main():
         from marlsoccer.config import load_config
         cfg = load_config()
         cfg["simulation"]["max_steps"] = args.max_steps
-    batch = SoccerBatch(E, config=cfg, device=dev.index)
+    ring = args.frame_ring
+    if ring and args.allgather:
+        raise SystemExit("--frame-ring and --allgather are exclusive")
+    batch = (FrameRingBatch(E, ring=ring, config=cfg, device=dev.index) if ring else
+             SoccerBatch(E, config=cfg, device=dev.index))
     batch.reset(seed=19 + rank * E)  # env i of rank r seeded 19 + r*E + i (global index)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
@@ -184,7 +194,8 @@ def main():
     if args.allgather and world > 1:
         gathered = torch.empty((world * E, 4, 66), dtype=torch.float32, device=dev)
 
-    launch = batch.launcher(actions, obs, rew, term, trunc, goal, score)
+    launch = (batch.launcher(actions, rew, term, trunc, goal, score) if ring else
+              batch.launcher(actions, obs, rew, term, trunc, goal, score))
 
     def one(i):
         launch(i)
@@ -229,7 +240,7 @@ def main():
     # obs all-gather after every step (BASELINE configs[3]; SURVEY.md 8(e) asks for the rate
     # with and without it). Reported beside `value`, which stays the no-collective rate.
     gather_report = None
-    if world > 1 and gathered is None and not shared:
+    if world > 1 and gathered is None and not shared and not ring:
         gbuf = torch.empty((world * E, 4, 66), dtype=torch.float32, device=dev)
         gk = min(200, args.steps)
         for i in range(5):
@@ -263,6 +274,10 @@ def main():
     stats = batch.stats()
     bytes_per_step = SURVEY_BYTES + 2 * ARB_BYTES * mean_arb
     layout_bytes = LAYOUT_READ + LAYOUT_WRITE + 2 * ARB_BYTES * mean_arb
+    if ring:
+        bytes_per_step = RING_BYTES + 2 * 352 / (ring - 2) + 2 * ARB_BYTES * mean_arb
+        # obs: one frame (+ two on a wrap) instead of three; the t-2 snapshot read only on a wrap
+        layout_bytes += (352 + 2 * 352 / (ring - 2)) - 1056 - 104 + 104 / (ring - 2)
     achieved = bytes_per_step * E / (kern_ms * 1e-3) / 1e9
     window = regime(args.warmup, args.steps, args.max_steps)
     steady = window.startswith("steady state")
@@ -271,7 +286,7 @@ def main():
         pmc = load_pmc_traffic()
         traffic = None
         pmc_info = None
-        if pmc and pmc.get("envs") == E:
+        if pmc and pmc.get("envs") == E and not ring:
             # HBM bytes per launch from the committed rocprofv3 PMC passes (a steady-state
             # window); divided by this run's kernel time only when this run timed the same regime
             pmc_info = {"source": f"profiles/{pmc['tag']}_pmc.json", "bytes_per_launch": pmc["hbm_bytes_per_launch"],
@@ -301,13 +316,18 @@ def main():
                                     " (BASELINE.json configs[4] per-GPU shard)" if E == 32768 and args.max_steps == 512
                                     else ""),
                        "envs_per_gpu": E, "global_envs": world * E, "max_steps": args.max_steps,
-                       "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else "")},
+                       "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else ""),
+                       **({"obs_layout": f"frame ring, R = {ring} (opt-in; obs is a strided (N, 4, 66) window)"}
+                          if ring else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "ms_step_kernel", "kernel_ms": kern_ms,
+                         "kernel": "ms_step_ring_kernel" if ring else "ms_step_kernel", "kernel_ms": kern_ms,
                          "kernel_ms_method": "HIP events around the K back-to-back launches / K",
                          "alg_bytes_per_env_step": bytes_per_step,
-                         "alg_bytes_source": "SURVEY.md §8(d): 2,289 + 2 x 20 B x mean cached arbiters",
+                         "alg_bytes_source": ("SURVEY.md §8(d) without the prior frames' read and re-write: 881 + "
+                                              f"2 x 352 B / (R - 2) wrap frames (R = {ring}) + 2 x 20 B x mean cached "
+                                              "arbiters") if ring else
+                                             "SURVEY.md §8(d): 2,289 + 2 x 20 B x mean cached arbiters",
                          "layout_bytes_per_env_step": layout_bytes,
                          "traffic_source": (pmc_info["source"] + " (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch) "
                                             "over this run's kernel_ms") if traffic is not None else
