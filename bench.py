@@ -65,6 +65,7 @@ def parse():
                     help="opt-in frame-ring observations (FrameRingBatch, R frames per agent ring); "
                          "default 0: the reference's contiguous (N, 4, 66) stacked obs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ring-leg", action="store_true", help="skip the frame-ring leg timed beside the headline")
     ap.add_argument("--cpu-envs", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target wall time of the all-cores CPU baseline (its step count is sized from the "
@@ -264,6 +265,28 @@ def main():
                          "collective": f"RCCL all_gather_into_tensor of obs, {E * 1056 / 1e6:.1f} MB per rank per step"}
         del gbuf
 
+    # The opt-in frame-ring layout timed beside the headline (N = 1, default run): same envs,
+    # seeds, actions and window on a FrameRingBatch with R = 32; reported as `frame_ring`, never
+    # as `value` (the reference's API hands back a contiguous stacked obs).
+    ring_report = None
+    if world == 1 and not ring and not args.no_ring_leg:
+        rb = FrameRingBatch(E, ring=32, config=cfg, device=dev.index)
+        rb.reset(seed=19)
+        rl = rb.launcher(actions, rb.rew, rb.term, rb.trunc, rb.goal, rb.score)
+        for i in range(args.warmup):
+            rl(i)
+        torch.cuda.synchronize()
+        r0 = time.perf_counter()
+        for i in range(args.steps):
+            rl(args.warmup + i)
+        torch.cuda.synchronize()
+        r_el = time.perf_counter() - r0
+        rb.close()
+        ring_report = {"value": E * args.steps / r_el, "unit": "env-steps/s", "ms_per_step": r_el * 1e3 / args.steps,
+                       "R": 32, "kernel": "ms_step_ring_kernel",
+                       "obs": "strided (N, 4, 66) window into a (N, 4, 32, 22) frame ring, same values as obs "
+                              "(bench.py --frame-ring 32 gives its roofline line)"}
+
     # cached arbiters per env (the cache bytes of the algorithmic count), sampled mid-episode:
     # 300 more untimed steps, so the sample is not the just-reset state at an episode boundary
     for i in range(300):
@@ -340,6 +363,8 @@ def main():
         }
         if gather_report is not None:
             line["with_obs_allgather"] = gather_report
+        if ring_report is not None:
+            line["frame_ring"] = ring_report
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args)
             cb["gpu_over_cpu"] = value / cb["value"]

@@ -208,6 +208,13 @@ struct Lds {
   uint32_t ch[KC][MS_BLOCK];
   float4 cj[KC][MS_BLOCK];
   float4 h1[7][MS_BLOCK];  // the t-1 snapshot (step-start state) across the physics
+  // static-agent pair tests shared out over the wave: task (owner lane << 5 | pair bit) and
+  // its Col result (count; n, p1[0]; p2[0], p1[1]; p2[1], hash[0], hash[1])
+  struct {
+    uint32_t task[MS_BLOCK];
+    int cnt[MS_BLOCK];
+    float4 res[3][MS_BLOCK];
+  } nt;
 };
 
 // body velocity (v, w) and bias velocity (vb, wb) of body b in LDS
@@ -633,12 +640,11 @@ struct Contacts {
 
 // d = c ? s : d, field by field with unconditional stores: a conditional whole-struct store
 // lets the optimizer merge the KREG stores into one store through a phi of slot pointers,
-// which pins the slots in scratch memory.
+// which pins the slots in scratch memory. Only the fields the narrowphase defines: u, nMass,
+// tMass, bias, bounce and jb are written by prestep_one before anything reads them.
 __device__ __forceinline__ void slot_select(CSlot& d, const CSlot& s, bool c) {
-  d.r1 = c ? s.r1 : d.r1; d.r2 = c ? s.r2 : d.r2; d.n = c ? s.n : d.n; d.u = c ? s.u : d.u;
-  d.nMass = c ? s.nMass : d.nMass; d.tMass = c ? s.tMass : d.tMass; d.bias = c ? s.bias : d.bias;
-  d.bounce = c ? s.bounce : d.bounce; d.jn = c ? s.jn : d.jn; d.jt = c ? s.jt : d.jt; d.jb = c ? s.jb : d.jb;
-  d.m = c ? s.m : d.m;
+  d.r1 = c ? s.r1 : d.r1; d.r2 = c ? s.r2 : d.r2; d.n = c ? s.n : d.n;
+  d.jn = c ? s.jn : d.jn; d.jt = c ? s.jt : d.jt; d.m = c ? s.m : d.m;
 }
 
 // overflow slots KREG..MAXC-1 live in the global spill buffer; only pile-ups reach them
@@ -669,6 +675,8 @@ __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds
   const int p = CS_PAIR(c.m);
   const float e_s = ((p - 10) & 7) < 6 ? P.e_aw : P.e_ag;
   const float e = p < 6 ? P.e_aa : (p < 10 ? P.e_ab : (p < 42 ? e_s : P.e_bw));
+  const float u_s = ((p - 10) & 7) < 6 ? P.u_aw : P.u_ag;
+  c.u = p < 6 ? P.u_aa : (p < 10 ? P.u_ab : (p < 42 ? u_s : P.u_bw));
   const V2 n = c.n;
   const V2 body_delta = L.ph.p[bb][lane] - L.ph.p[ba][lane];
   V2 va, vb;
@@ -750,6 +758,11 @@ __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int
   st_v(L, bb, lane, vmadd(j, mb, vb), __builtin_fmaf(ib, vcross(r2, j), wb_));
 }
 
+// number of set bits of m below this lane
+__device__ __forceinline__ int lane_rank(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ __forceinline__ void lds_box(const Lds& L, int i, int lane, Box& b) {
   const F4 t = lds_f4(&L.ph.box[i][lane]);
   box_world(t.x, t.y, t.z, t.w, b);
@@ -807,7 +820,7 @@ __device__ __forceinline__ void cache_age_current(At a, const Lds& L, CacheWalk&
 
 // cpSpaceCollideShapes + cpArbiterUpdate for one touching pair
 __device__ __forceinline__ void add_arbiter(At a, const Lds& L, Contacts& C, CSlot* ovf, CacheWalk& W, int p, int ba,
-                                            int bb, const Col& col, float u, unsigned long long* overflow_acc) {
+                                            int bb, const Col& col, unsigned long long* overflow_acc) {
   const int lane = a.lane;
   if (C.na >= MAXA) { (*overflow_acc)++; return; }
   while (cur_pair(a, W) < p) cache_age_current(a, L, W, overflow_acc);
@@ -837,8 +850,7 @@ __device__ __forceinline__ void add_arbiter(At a, const Lds& L, Contacts& C, CSl
       const int h = col.hash[k];
       s.r1 = vsub(col.p1[k], pa);
       s.r2 = vsub(col.p2[k], pb);
-      s.n = col.n; s.u = u;
-      s.nMass = 0.0f; s.tMass = 0.0f; s.bias = 0.0f; s.bounce = 0.0f; s.jb = 0.0f;
+      s.n = col.n;
       float jn = 0.0f, jt = 0.0f;
       if (ocount > 0 && oh0 == h) { jn = oj[0]; jt = oj[1]; }
       if (ocount > 1 && oh1 == h) { jn = oj[2]; jt = oj[3]; }
@@ -963,7 +975,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     col_box_box(A, B, col);
     ACC_END(aa_col);
     ACC_BEGIN(aa_add);
-    if (col.count) add_arbiter(a, L, C, ovf, W, p, i, j, col, P.u_aa, overflow_acc);
+    if (col.count) add_arbiter(a, L, C, ovf, W, p, i, j, col, overflow_acc);
     ACC_END(aa_add);
     ACC_INC(aa_n);
   }
@@ -974,24 +986,75 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     lds_box(L, i, lane, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     col_circle_box(ballc, BR, B, col);
-    if (col.count) add_arbiter(a, L, C, ovf, W, 6 + i, 4, i, col, P.u_ab, overflow_acc);
+    if (col.count) add_arbiter(a, L, C, ovf, W, 6 + i, 4, i, col, overflow_acc);
   }
   STAMP(11);
-  while (mSA) {
-    const int q = __builtin_ctz(mSA);
-    mSA &= mSA - 1;
-    const int i = q >> 3, s = q & 7;
-    Box B;
-    lds_box(L, i, lane, B);
-    Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
-    const Seg sg = L.seg[s];
-    ACC_BEGIN(sa_col);
-    col_seg_box(sg, B, col);
-    ACC_END(sa_col);
-    ACC_BEGIN(sa_add);
-    if (col.count) add_arbiter(a, L, C, ovf, W, 10 + q, 5, i, col, s < 6 ? P.u_aw : P.u_ag, overflow_acc);
-    ACC_END(sa_add);
-    ACC_INC(sa_n);
+  // Static-agent pairs: the tests (col_seg_box, the costly part) are spread over the wave's
+  // active lanes instead of run by each env's lane in turn — a lane whose env has k touching
+  // pairs would otherwise hold the wave for k tests while the others idle. Tasks are numbered in
+  // (lane, ctz) order; each window of `nact` tasks is tested by the active lanes (rank r takes
+  // task base + r), then every lane inserts its own results in ctz order, so the arbiter order
+  // and every value are those of the per-lane loop. Prefix sums by bit-sliced ballots (exact
+  // with inactive lanes, which hold no tasks).
+  {
+    const uint64_t act = __builtin_amdgcn_read_exec();
+    const int nact = __builtin_popcountll(act);
+    const int rank = lane_rank(act);
+    const int cnt = __builtin_popcount(mSA);
+    int pre = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const uint64_t m = __ballot((cnt >> b) & 1);
+      pre += lane_rank(m) << b;
+      total += __builtin_popcountll(m) << b;
+    }
+    int tf = pre, tc = pre;  // global index of this lane's next task to post / to insert
+    uint32_t mf = mSA, mc = mSA;
+    for (int base = 0; base < total; base += nact) {
+      while (mf && tf < base + nact) {
+        const int q = __builtin_ctz(mf);
+        mf &= mf - 1;
+        L.nt.task[tf - base] = (uint32_t)(lane << 5) | (uint32_t)q;
+        ++tf;
+      }
+      asm volatile("" ::: "memory");
+      ACC_BEGIN(sa_col);
+      if (rank < total - base) {
+        const uint32_t v = L.nt.task[rank];
+        const int q = (int)(v & 31u);
+        Box B;
+        lds_box(L, q >> 3, (int)(v >> 5), B);
+        Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
+        const Seg sg = L.seg[q & 7];
+        col_seg_box(sg, B, col);
+        L.nt.cnt[rank] = col.count;
+        L.nt.res[0][rank] = make_float4(col.n.x, col.n.y, col.p1[0].x, col.p1[0].y);
+        L.nt.res[1][rank] = make_float4(col.p2[0].x, col.p2[0].y, col.p1[1].x, col.p1[1].y);
+        L.nt.res[2][rank] = make_float4(col.p2[1].x, col.p2[1].y, __int_as_float(col.hash[0]), __int_as_float(col.hash[1]));
+      }
+      ACC_END(sa_col);
+      asm volatile("" ::: "memory");
+      ACC_BEGIN(sa_add);
+      while (mc && tc < base + nact) {
+        const int q = __builtin_ctz(mc);
+        mc &= mc - 1;
+        const int t = tc - base, i = q >> 3;
+        ++tc;
+        Col col;
+        col.count = L.nt.cnt[t];
+        if (col.count) {
+          const F4 r0 = lds_f4(&L.nt.res[0][t]), r1 = lds_f4(&L.nt.res[1][t]), r2 = lds_f4(&L.nt.res[2][t]);
+          col.n = v2(r0.x, r0.y);
+          col.p1[0] = v2(r0.z, r0.w); col.p2[0] = v2(r1.x, r1.y);
+          col.p1[1] = v2(r1.z, r1.w); col.p2[1] = v2(r2.x, r2.y);
+          col.hash[0] = __float_as_int(r2.z); col.hash[1] = __float_as_int(r2.w);
+          add_arbiter(a, L, C, ovf, W, 10 + q, 5, i, col, overflow_acc);
+        }
+        ACC_INC(sa_n);
+      }
+      ACC_END(sa_add);
+      asm volatile("" ::: "memory");
+    }
   }
   STAMP(13);
   while (mBS) {
@@ -1000,7 +1063,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     const Seg sg = L.seg[s];
     col_circle_seg(ballc, BR, sg, col);
-    if (col.count) add_arbiter(a, L, C, ovf, W, 42 + s, 4, 5, col, P.u_bw, overflow_acc);
+    if (col.count) add_arbiter(a, L, C, ovf, W, 42 + s, 4, 5, col, overflow_acc);
   }
   while (W.cur < W.nc_old) cache_age_current(a, L, W, overflow_acc);
   STAMP(3);
