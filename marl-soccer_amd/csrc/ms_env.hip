@@ -195,6 +195,7 @@ __device__ __forceinline__ void store_rng(At a, Env& E) {
 // x/y pairs are stored together so that they load into register pairs for packed math.
 
 constexpr int KC = 4;  // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (pile-ups)
+constexpr int NLDS = 2;  // overflow contacts staged in LDS during the solver (union with the narrowphase scratch)
 
 struct Lds {
   Seg seg[8];  // static segments (walls, goal lines), read with per-lane indices
@@ -204,17 +205,24 @@ struct Lds {
     float4 bw[6][MS_BLOCK];        // bias velocity x, y, bias angular velocity
     float4 box[4][MS_BLOCK];  // agent box transform (px, py, cos, sin): one 16-B read per box
   } ph;
-  // previous step's arbiter cache, entries 0..KC-1 (loaded with the state at kernel start)
-  uint32_t ch[KC][MS_BLOCK];
-  float4 cj[KC][MS_BLOCK];
   float4 h1[7][MS_BLOCK];  // the t-1 snapshot (step-start state) across the physics
-  // static-agent pair tests shared out over the wave: task (owner lane << 5 | pair bit) and
-  // its Col result (count; n, p1[0]; p2[0], p1[1]; p2[1], hash[0], hash[1])
-  struct {
-    uint32_t task[MS_BLOCK];
-    int cnt[MS_BLOCK];
-    float4 res[3][MS_BLOCK];
-  } nt;
+  union {
+    struct {
+      // previous step's arbiter cache, entries 0..KC-1 (loaded with the state at kernel start)
+      uint32_t ch[KC][MS_BLOCK];
+      float4 cj[KC][MS_BLOCK];
+      // static-agent pair tests shared out over the wave: task (owner lane << 5 | pair bit)
+      // and its Col result (count; n, p1[0]; p2[0], p1[1]; p2[1], hash[0], hash[1])
+      struct {
+        uint32_t task[MS_BLOCK];
+        int cnt[MS_BLOCK];
+        float4 res[3][MS_BLOCK];
+      } nt;
+    } np;  // narrowphase
+    // prestep, warm start, solver: contacts KREG .. KREG+NLDS-1 (pile-ups), four 16-B records
+    // (r1, r2 | n, u, nMass | tMass, bias, bounce, jn | jt, jb, m, -) per lane
+    float4 ov[NLDS][4][MS_BLOCK];
+  } u;
 };
 
 // body velocity (v, w) and bias velocity (vb, wb) of body b in LDS
@@ -656,6 +664,28 @@ __device__ __forceinline__ void slot_put(Contacts& C, CSlot* ovf, int k, const C
   if (k >= KREG) ovf[k - KREG] = s;
 }
 
+// overflow contact KREG + j staged in LDS (Lds::u.ov) for prestep, warm start and solver
+__device__ __forceinline__ void ov_get(const Lds& L, int j, int lane, CSlot& c) {
+  const F4 q0 = lds_f4(&L.u.ov[j][0][lane]), q1 = lds_f4(&L.u.ov[j][1][lane]);
+  const F4 q2 = lds_f4(&L.u.ov[j][2][lane]), q3 = lds_f4(&L.u.ov[j][3][lane]);
+  c.r1 = v2(q0.x, q0.y); c.r2 = v2(q0.z, q0.w); c.n = v2(q1.x, q1.y); c.u = q1.z; c.nMass = q1.w;
+  c.tMass = q2.x; c.bias = q2.y; c.bounce = q2.z; c.jn = q2.w;
+  c.jt = q3.x; c.jb = q3.y; c.m = __float_as_uint(q3.z);
+}
+__device__ __forceinline__ void ov_put(Lds& L, int j, int lane, const CSlot& c) {
+  L.u.ov[j][0][lane] = make_float4(c.r1.x, c.r1.y, c.r2.x, c.r2.y);
+  L.u.ov[j][1][lane] = make_float4(c.n.x, c.n.y, c.u, c.nMass);
+  L.u.ov[j][2][lane] = make_float4(c.tMass, c.bias, c.bounce, c.jn);
+  L.u.ov[j][3][lane] = make_float4(c.jt, c.jb, __uint_as_float(c.m), 0.0f);
+}
+// contact k >= KREG after the solver: from LDS or from the global spill
+__device__ __forceinline__ CSlot over_slot(const Lds& L, int lane, const CSlot* ovf, int k) {
+  CSlot c;
+  if (k < KREG + NLDS) ov_get(L, k - KREG, lane, c);
+  else c = ovf[k - KREG];
+  return c;
+}
+
 // per-body inverse mass / moment without a per-lane indexed parameter load
 __device__ __forceinline__ float body_minv(const Params& P, int b) {
   return b < 4 ? P.m_inv[0] : (b == 4 ? P.m_inv[4] : 0.0f);
@@ -783,11 +813,11 @@ __device__ __forceinline__ uint32_t cache_key(uint32_t hdr) { return (hdr & 63u)
 // (the HBM fallback reads through address-space-1 pointers: with generic pointers the optimizer
 // merges the LDS and the global read into one flat-address load through a selected address)
 __device__ __forceinline__ uint32_t old_hdr(At a, const Lds& L, int par, int k) {
-  if (k < KC) return L.ch[k][a.lane];
+  if (k < KC) return L.u.np.ch[k][a.lane];
   return __builtin_nontemporal_load((gu32_t*)plane<uint32_t>(a, OFF_CH, par * MAXA + k));
 }
 __device__ __forceinline__ float4 old_imp(At a, const Lds& L, int par, int k) {
-  if (k < KC) return L.cj[k][a.lane];
+  if (k < KC) return L.u.np.cj[k][a.lane];
   gu32_t* g = (gu32_t*)plane<float4>(a, OFF_CJ, par * MAXA + k);
   return make_float4(__uint_as_float(__builtin_nontemporal_load(g)), __uint_as_float(__builtin_nontemporal_load(g + 1)),
                      __uint_as_float(__builtin_nontemporal_load(g + 2)), __uint_as_float(__builtin_nontemporal_load(g + 3)));
@@ -882,8 +912,15 @@ __device__ __forceinline__ void write_arbiter_cache(At a, int npar, const CSlot&
       }                                                               \
     });                                                               \
     for (int k_ = KREG; k_ < (C).nc; ++k_) {                          \
-      CSlot& c_ = (OVF)[k_ - KREG];                                   \
-      BODY;                                                           \
+      if (k_ < KREG + NLDS) {                                         \
+        CSlot c_;                                                     \
+        ov_get(L, k_ - KREG, lane, c_);                               \
+        BODY;                                                         \
+        ov_put(L, k_ - KREG, lane, c_);                               \
+      } else {                                                        \
+        CSlot& c_ = (OVF)[k_ - KREG];                                 \
+        BODY;                                                         \
+      }                                                               \
     }                                                                 \
   }
 
@@ -1014,23 +1051,23 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
       while (mf && tf < base + nact) {
         const int q = __builtin_ctz(mf);
         mf &= mf - 1;
-        L.nt.task[tf - base] = (uint32_t)(lane << 5) | (uint32_t)q;
+        L.u.np.nt.task[tf - base] = (uint32_t)(lane << 5) | (uint32_t)q;
         ++tf;
       }
       asm volatile("" ::: "memory");
       ACC_BEGIN(sa_col);
       if (rank < total - base) {
-        const uint32_t v = L.nt.task[rank];
+        const uint32_t v = L.u.np.nt.task[rank];
         const int q = (int)(v & 31u);
         Box B;
         lds_box(L, q >> 3, (int)(v >> 5), B);
         Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
         const Seg sg = L.seg[q & 7];
         col_seg_box(sg, B, col);
-        L.nt.cnt[rank] = col.count;
-        L.nt.res[0][rank] = make_float4(col.n.x, col.n.y, col.p1[0].x, col.p1[0].y);
-        L.nt.res[1][rank] = make_float4(col.p2[0].x, col.p2[0].y, col.p1[1].x, col.p1[1].y);
-        L.nt.res[2][rank] = make_float4(col.p2[1].x, col.p2[1].y, __int_as_float(col.hash[0]), __int_as_float(col.hash[1]));
+        L.u.np.nt.cnt[rank] = col.count;
+        L.u.np.nt.res[0][rank] = make_float4(col.n.x, col.n.y, col.p1[0].x, col.p1[0].y);
+        L.u.np.nt.res[1][rank] = make_float4(col.p2[0].x, col.p2[0].y, col.p1[1].x, col.p1[1].y);
+        L.u.np.nt.res[2][rank] = make_float4(col.p2[1].x, col.p2[1].y, __int_as_float(col.hash[0]), __int_as_float(col.hash[1]));
       }
       ACC_END(sa_col);
       asm volatile("" ::: "memory");
@@ -1041,9 +1078,9 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
         const int t = tc - base, i = q >> 3;
         ++tc;
         Col col;
-        col.count = L.nt.cnt[t];
+        col.count = L.u.np.nt.cnt[t];
         if (col.count) {
-          const F4 r0 = lds_f4(&L.nt.res[0][t]), r1 = lds_f4(&L.nt.res[1][t]), r2 = lds_f4(&L.nt.res[2][t]);
+          const F4 r0 = lds_f4(&L.u.np.nt.res[0][t]), r1 = lds_f4(&L.u.np.nt.res[1][t]), r2 = lds_f4(&L.u.np.nt.res[2][t]);
           col.n = v2(r0.x, r0.y);
           col.p1[0] = v2(r0.z, r0.w); col.p2[0] = v2(r1.x, r1.y);
           col.p1[1] = v2(r1.z, r1.w); col.p2[1] = v2(r2.x, r2.y);
@@ -1066,6 +1103,10 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     if (col.count) add_arbiter(a, L, C, ovf, W, 42 + s, 4, 5, col, overflow_acc);
   }
   while (W.cur < W.nc_old) cache_age_current(a, L, W, overflow_acc);
+  // contacts KREG.. of a pile-up from the global spill into LDS for the 12 passes over them
+  // (the narrowphase scratch they share LDS with is dead from here on)
+  asm volatile("" ::: "memory");
+  for (int k = KREG; k < C.nc && k < KREG + NLDS; ++k) ov_put(L, k - KREG, lane, ovf[k - KREG]);
   STAMP(3);
 #ifdef MS_STAMPS
   ACC_STORE(aa_col, 16); ACC_STORE(aa_add, 17); ACC_STORE(aa_n, 18);
@@ -1130,13 +1171,13 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     });
     if (KREG - 1 < C.nc) {
       CSlot next = C.reg[KREG - 1];
-      if (KREG < C.nc) next = ovf[0];
+      if (KREG < C.nc) next = over_slot(L, lane, ovf, KREG);
       write_arbiter_cache(a, W.par ^ 1, C.reg[KREG - 1], next);
     }
     // the contact after the last one is never read (count > 1 only for an arbiter's first contact,
     // whose second contact exists); k + 1 stays inside the env's spill slice
     for (int k = KREG; k < C.nc; ++k)
-      write_arbiter_cache(a, W.par ^ 1, ovf[k - KREG], ovf[k + 1 < MAXC ? k + 1 - KREG : k - KREG]);
+      write_arbiter_cache(a, W.par ^ 1, over_slot(L, lane, ovf, k), over_slot(L, lane, ovf, k + 1 < MAXC ? k + 1 : k));
   }
   STAMP(6);
   const int nn = W.out < MAXA ? W.out : MAXA;
@@ -1240,8 +1281,8 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   uint32_t pk0 = 0u;
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
-    L.ch[k][lane] = pch[k];
-    L.cj[k][lane] = pcj[k];
+    L.u.np.ch[k][lane] = pch[k];
+    L.u.np.cj[k][lane] = pcj[k];
     pk0 |= cache_key(pch[k]) << (8 * k);
   }
 
