@@ -195,7 +195,7 @@ __device__ __forceinline__ void store_rng(At a, Env& E) {
 // x/y pairs are stored together so that they load into register pairs for packed math.
 
 constexpr int KC = 4;  // old arbiter-cache entries staged in LDS; entries KC.. are read from HBM (pile-ups)
-constexpr int NLDS = 2;  // overflow contacts staged in LDS during the solver (union with the narrowphase scratch)
+constexpr int NLDS = 3;  // overflow contacts staged in LDS during the solver (union with the narrowphase scratch)
 
 struct Lds {
   Seg seg[8];  // static segments (walls, goal lines), read with per-lane indices
@@ -212,10 +212,10 @@ struct Lds {
       uint32_t ch[KC][MS_BLOCK];
       float4 cj[KC][MS_BLOCK];
       // static-agent pair tests shared out over the wave: task (owner lane << 5 | pair bit)
-      // and its Col result (count; n, p1[0]; p2[0], p1[1]; p2[1], hash[0], hash[1])
+      // and its Col result (n, p1[0]; p2[0], p1[1]; p2[1], hash[0] | count << 16, hash[1]);
+      // feature hashes are 8-bit (MS_FEATURE_HASH)
       struct {
         uint32_t task[MS_BLOCK];
-        int cnt[MS_BLOCK];
         float4 res[3][MS_BLOCK];
       } nt;
     } np;  // narrowphase
@@ -1064,10 +1064,10 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
         Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
         const Seg sg = L.seg[q & 7];
         col_seg_box(sg, B, col);
-        L.u.np.nt.cnt[rank] = col.count;
         L.u.np.nt.res[0][rank] = make_float4(col.n.x, col.n.y, col.p1[0].x, col.p1[0].y);
         L.u.np.nt.res[1][rank] = make_float4(col.p2[0].x, col.p2[0].y, col.p1[1].x, col.p1[1].y);
-        L.u.np.nt.res[2][rank] = make_float4(col.p2[1].x, col.p2[1].y, __int_as_float(col.hash[0]), __int_as_float(col.hash[1]));
+        L.u.np.nt.res[2][rank] = make_float4(col.p2[1].x, col.p2[1].y, __int_as_float((col.count ? col.hash[0] & 0xffff : 0) | (col.count << 16)),
+                                             __int_as_float(col.hash[1]));
       }
       ACC_END(sa_col);
       asm volatile("" ::: "memory");
@@ -1077,14 +1077,15 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
         mc &= mc - 1;
         const int t = tc - base, i = q >> 3;
         ++tc;
+        // one round trip: the count travels with the hashes
+        const F4 r0 = lds_f4(&L.u.np.nt.res[0][t]), r1 = lds_f4(&L.u.np.nt.res[1][t]), r2 = lds_f4(&L.u.np.nt.res[2][t]);
         Col col;
-        col.count = L.u.np.nt.cnt[t];
+        col.count = __float_as_int(r2.z) >> 16;
         if (col.count) {
-          const F4 r0 = lds_f4(&L.u.np.nt.res[0][t]), r1 = lds_f4(&L.u.np.nt.res[1][t]), r2 = lds_f4(&L.u.np.nt.res[2][t]);
           col.n = v2(r0.x, r0.y);
           col.p1[0] = v2(r0.z, r0.w); col.p2[0] = v2(r1.x, r1.y);
           col.p1[1] = v2(r1.z, r1.w); col.p2[1] = v2(r2.x, r2.y);
-          col.hash[0] = __float_as_int(r2.z); col.hash[1] = __float_as_int(r2.w);
+          col.hash[0] = __float_as_int(r2.z) & 0xffff; col.hash[1] = __float_as_int(r2.w);
           add_arbiter(a, L, C, ovf, W, 10 + q, 5, i, col, overflow_acc);
         }
         ACC_INC(sa_n);
