@@ -634,6 +634,7 @@ struct CSlot {
 
 constexpr int KREG = 8;  // contacts held in registers; further ones go to the global spill (pile-ups)
 constexpr int PRE_GROUP = 2;  // register slots per wave-uniform prestep group (2: 53.3 us, 4: 53.7, 8: 54.3, per-lane: 53.9)
+static_assert(KREG % PRE_GROUP == 0, "prestep groups must cover every register slot");
 #define MAXC (2 * MAXA)                 // contact capacity (2 per arbiter)
 
 __device__ __forceinline__ void cache_write(At a, int par, int k, uint32_t hdr, float4 j) {
