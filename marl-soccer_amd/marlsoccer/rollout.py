@@ -43,11 +43,12 @@ class RunningMeanStd:
         batch_count = x.shape[0]
         delta = batch_mean - self.mean
         tot_count = self.count + batch_count
-        self.mean = self.mean + delta * batch_count / tot_count
         m_a = self.var * self.count
         m_b = batch_var * batch_count
         m2 = m_a + m_b + torch.square(delta) * self.count * batch_count / tot_count
-        self.var = m2 / tot_count
+        # in place: a captured rollout graph (DeviceRollout(graph=True)) reads these tensors
+        self.mean.copy_(self.mean + delta * batch_count / tot_count)
+        self.var.copy_(m2 / tot_count)
         self.count = tot_count
 
     @property
@@ -106,11 +107,17 @@ class Agent(nn.Module):
         action_mean = self.actor_mean(x)
         action_std = torch.exp(self.actor_logstd.expand_as(action_mean))
         if action is None:
-            action = torch.normal(action_mean, action_std, generator=generator)
+            # torch.normal(mean, std, generator) computed as its kernels do (a standard normal
+            # draw, times std, plus mean) without its host-side check that std >= 0, which
+            # synchronises and cannot run inside a captured graph
+            eps = torch.randn(action_mean.shape, device=action_mean.device, generator=generator)
+            action = eps * action_std + action_mean
         else:
             z = (torch.rand(action_mean.shape, device=action_mean.device, generator=generator) * 2 - 1) * self.rpo_alpha
             action_mean = action_mean + z
-        probs = Normal(action_mean, action_std)
+        # no argument validation: it synchronises with the host (twice per call), which costs a
+        # stall per rollout step and is not allowed inside a captured graph; values are unchanged
+        probs = Normal(action_mean, action_std, validate_args=False)
         return action, probs.log_prob(action).sum(1), probs.entropy().sum(1), self.critic(x)
 
     def get_deterministic_action(self, x: torch.Tensor) -> torch.Tensor:
@@ -125,14 +132,22 @@ class DeviceRollout:
     notebook's, plus next_obs / next_done for bootstrapping, the number of finished env
     episodes and the sum of their final (blue, red) scores.
     deterministic=True uses the actor mean (eval.py:79-81) instead of sampling.
+    graph=True: the first collect() runs eagerly (it also initialises the GEMM libraries); the
+    second captures its num_steps steps as one HIP graph and replays it, and later calls replay
+    that graph — one launch per rollout instead of ~40 kernel launches per step. The captured
+    graph reads the agent's parameters and the normalizer's mean/var in place, so the PPO
+    update must modify them in place (optimizer steps and RunningMeanStd.update do).
     """
 
     def __init__(self, batch, agent: Agent, normalizer: RunningMeanStd, num_steps: int, seed: int = 0,
-                 deterministic: bool = False, update_normalizer: bool = True):
+                 deterministic: bool = False, update_normalizer: bool = True, graph: bool = False):
         self.batch, self.agent, self.normalizer = batch, agent, normalizer
         self.T, self.N = int(num_steps), batch.num_envs
         self.deterministic = deterministic
         self.update_normalizer = update_normalizer
+        self.graph = graph
+        self._graph = None
+        self._collects = 0
         dev = batch.device
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed)
@@ -176,9 +191,34 @@ class DeviceRollout:
         self.episodes += finished.sum()
         self.score_sum += (b.score * finished[:, None]).sum(dim=0)
 
-    def collect(self) -> dict:
+    def _run_steps(self) -> None:
         for t in range(self.T):
             self.step(t)
+
+    def _capture(self) -> None:
+        b, dev = self.batch, self.batch.device
+        g = torch.cuda.CUDAGraph()
+        g.register_generator_state(self.gen)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        old = b.stream
+        b.set_stream(s)  # ms_step launches on the capture stream
+        try:
+            with torch.cuda.graph(g, stream=s):
+                self._run_steps()
+        finally:
+            b.set_stream(old)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        self._graph = g
+
+    def collect(self) -> dict:
+        if self.graph and self._collects > 0:
+            if self._graph is None:
+                self._capture()  # records only; the replay below runs it
+            self._graph.replay()
+        else:
+            self._run_steps()
+        self._collects += 1
         # the policy's actions are checked once per rollout (one synchronisation): a non-finite
         # action raises the reference's ValueError (soccer_env.py:116-117)
         self.batch.raise_if_nonfinite()

@@ -98,6 +98,48 @@ def test_device_rollout_drives_env_on_gpu():
 
 
 @pytest.mark.gpu
+def test_graph_rollout_matches_eager_rollout():
+    """DeviceRollout(graph=True) (eager first collect, then one captured graph per rollout) ==
+    the eager rollout from the same state and seeds: storage, env outputs, normaliser, counters,
+    across three collects (eager, capture + replay, replay) with the normaliser updated between."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer import SoccerBatch
+    N, T = 256, 16
+    torch.manual_seed(0)
+    agent = Agent().cuda()
+    # the capturable sampling (standard normal x std + mean) draws what torch.normal draws
+    m = torch.randn((4096, 3), device="cuda")
+    s = torch.rand((4096, 3), device="cuda") + 0.1
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    want = torch.normal(m, s, generator=g)
+    g.manual_seed(3)
+    assert torch.equal(torch.randn(m.shape, device="cuda", generator=g) * s + m, want)
+    runs = []
+    for graph in (False, True):
+        b = SoccerBatch(N)
+        b.reset(seed=23)
+        rms = RunningMeanStd((66,), device="cuda")
+        ro = DeviceRollout(b, agent, rms, T, seed=11, graph=graph)
+        outs = []
+        for _ in range(3):
+            out = ro.collect()
+            outs.append({k: v.clone() for k, v in out.items()})
+        torch.cuda.synchronize()
+        runs.append((outs, rms.mean.clone(), rms.var.clone(), b.obs.clone(), b.score.clone(), b))
+    (oe, me, ve, obe, se, be), (og, mg, vg, obg, sg, bg) = runs
+    for a, g in zip(oe, og):
+        for k in a:
+            assert torch.equal(a[k], g[k]), k
+    assert torch.equal(me, mg) and torch.equal(ve, vg)
+    assert torch.equal(obe, obg) and torch.equal(se, sg)
+    assert bg._h is not None and bg.stream == torch.cuda.current_stream()
+    be.close()
+    bg.close()
+
+
+@pytest.mark.gpu
 def test_device_rollout_deterministic_matches_host_loop():
     """Deterministic rollout == the eval.py-style host loop (policy mean for blue, the same
     red actions) step for step."""

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput of the device-resident PPO rollout: env + policy.
 
-    python tools/bench_rollout.py [--envs 65536] [--steps 64] [--warmup 8]
+    python tools/bench_rollout.py [--envs 65536] [--steps 64] [--warmup 8] [--graph]
 
 One rollout step = normalise the blue agents' obs, actor + critic MLP forward (the
 reference's 66-512-256-128-64 tanh networks, fp32, random init), sample actions, draw the red
@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--graph", action="store_true",
+                    help="DeviceRollout(graph=True): time a replay of the captured rollout graph")
     a = ap.parse_args()
     import torch
     from marlsoccer import SoccerBatch
@@ -39,6 +41,24 @@ def main():
     rms = RunningMeanStd((66,), device="cuda")
     warm = DeviceRollout(b, agent, rms, a.warmup, seed=1, update_normalizer=False)
     warm.collect()
+    if a.graph:
+        ro = DeviceRollout(b, agent, rms, a.steps, seed=2, graph=True)
+        ro.collect()  # eager
+        ro.collect()  # capture + first replay
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ro.collect()  # replay
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(json.dumps({
+            "metric": "rollout env-steps/s (policy + env on device, one HIP graph per rollout)",
+            "value": a.envs * a.steps / dt, "unit": "env-steps/s", "envs": a.envs, "steps": a.steps,
+            "ms_per_step": dt * 1e3 / a.steps,
+            "policy": "Agent 66-512-256-128-64-{3,1} tanh x2, fp32, sampled actions; red uniform(-1,1)",
+            "timed": "third collect(): a replay of the graph captured by the second (normaliser update included)",
+        }))
+        b.close()
+        return
     ro = DeviceRollout(b, agent, rms, a.steps, seed=2)
     # env-kernel share: events around every ms_step of the timed rollout
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
