@@ -208,3 +208,46 @@ def test_batched_eval_matches_sequential_eval_loop():
         env.close()
         np.testing.assert_array_equal(res["returns"][i], ret)
         assert (int(res["score"][i, 0]), int(res["score"][i, 1])) == (score["blue"], score["red"])
+
+
+@pytest.mark.gpu
+def test_bf16_policy_rollout_within_bound_and_graph_equal():
+    """DeviceRollout(policy_dtype=bfloat16) (opt-in): the first step's actor mean and value are
+    within 2e-4 / 2e-2 of the fp32 rollout's on the same observations (bound stated in
+    DeviceRollout's docstring; measured ≈5e-5 / 5e-3 in DESIGN §10a), and its graph replay is
+    bit-identical to its eager loop."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer import SoccerBatch
+    N, T = 256, 8
+    torch.manual_seed(0)
+    agent = Agent().cuda()
+    firsts = {}
+    for dt in (torch.float32, torch.bfloat16):
+        b = SoccerBatch(N)
+        b.reset(seed=31)
+        ro = DeviceRollout(b, agent, RunningMeanStd((66,), device="cuda"), T, seed=4, deterministic=True,
+                           update_normalizer=False, policy_dtype=dt)
+        out = ro.collect()
+        firsts[dt] = (out["actions"][0].clone(), out["values"][0].clone())
+        b.close()
+    a32, v32 = firsts[torch.float32]
+    a16, v16 = firsts[torch.bfloat16]
+    assert a16.dtype == torch.float32 and v16.dtype == torch.float32
+    assert float((a16 - a32).abs().max()) <= 2e-4
+    assert float((v16 - v32).abs().max()) <= 2e-2
+    runs = []
+    for graph in (False, True):
+        b = SoccerBatch(N)
+        b.reset(seed=31)
+        ro = DeviceRollout(b, agent, RunningMeanStd((66,), device="cuda"), T, seed=4, graph=graph,
+                           policy_dtype=torch.bfloat16)
+        runs.append([{k: v.clone() for k, v in ro.collect().items()} for _ in range(3)])
+        b.close()
+    for a, g in zip(*runs):
+        for k in a:
+            assert torch.equal(a[k], g[k]), k
+    b = SoccerBatch(64)
+    with pytest.raises(ValueError):
+        DeviceRollout(b, agent, RunningMeanStd((66,), device="cuda"), 2, policy_dtype=torch.float16)
+    b.close()

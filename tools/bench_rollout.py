@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput of the device-resident PPO rollout: env + policy.
 
-    python tools/bench_rollout.py [--envs 65536] [--steps 64] [--warmup 8] [--graph]
+    python tools/bench_rollout.py [--envs 65536] [--steps 64] [--warmup 8] [--graph] [--bf16]
 
 One rollout step = normalise the blue agents' obs, actor + critic MLP forward (the
 reference's 66-512-256-128-64 tanh networks, fp32, random init), sample actions, draw the red
@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--graph", action="store_true",
                     help="DeviceRollout(graph=True): time a replay of the captured rollout graph")
+    ap.add_argument("--bf16", action="store_true", help="DeviceRollout(policy_dtype=torch.bfloat16) (opt-in)")
     a = ap.parse_args()
     import torch
     from marlsoccer import SoccerBatch
@@ -42,7 +43,8 @@ def main():
     warm = DeviceRollout(b, agent, rms, a.warmup, seed=1, update_normalizer=False)
     warm.collect()
     if a.graph:
-        ro = DeviceRollout(b, agent, rms, a.steps, seed=2, graph=True)
+        ro = DeviceRollout(b, agent, rms, a.steps, seed=2, graph=True,
+                           policy_dtype=torch.bfloat16 if a.bf16 else torch.float32)
         ro.collect()  # eager
         ro.collect()  # capture + first replay
         torch.cuda.synchronize()
@@ -54,12 +56,13 @@ def main():
             "metric": "rollout env-steps/s (policy + env on device, one HIP graph per rollout)",
             "value": a.envs * a.steps / dt, "unit": "env-steps/s", "envs": a.envs, "steps": a.steps,
             "ms_per_step": dt * 1e3 / a.steps,
-            "policy": "Agent 66-512-256-128-64-{3,1} tanh x2, fp32, sampled actions; red uniform(-1,1)",
+            "policy": "Agent 66-512-256-128-64-{3,1} tanh x2, " + ("bf16 autocast GEMMs" if a.bf16 else "fp32")
+                      + ", sampled actions; red uniform(-1,1)",
             "timed": "third collect(): a replay of the graph captured by the second (normaliser update included)",
         }))
         b.close()
         return
-    ro = DeviceRollout(b, agent, rms, a.steps, seed=2)
+    ro = DeviceRollout(b, agent, rms, a.steps, seed=2, policy_dtype=torch.bfloat16 if a.bf16 else torch.float32)
     # env-kernel share: events around every ms_step of the timed rollout
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     step_into = b.step_into
