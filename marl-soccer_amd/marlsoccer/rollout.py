@@ -144,8 +144,8 @@ class DeviceRollout:
     deterministic=True uses the actor mean (eval.py:79-81) instead of sampling.
     policy_dtype=torch.bfloat16 (opt-in; the notebook's policy is fp32, the default): the actor
     and critic GEMMs run under bf16 autocast (fp32 accumulation; normalisation, sampling,
-    log-probs and storage stay fp32) — about half the forward's time, with the action mean
-    within ≈1e-4 and the value within ≈1e-2 of fp32 (tests/test_policy.py states the bound).
+    log-probs and storage stay fp32) — about half the forward's time; the action mean stays
+    within 2e-4 and the value within 2e-2 of fp32 (the bound tests/test_policy.py asserts).
     graph=True: the first collect() runs eagerly (it also initialises the GEMM libraries); the
     second captures its num_steps steps as one HIP graph and replays it, and later calls replay
     that graph — one launch per rollout instead of ~40 kernel launches per step. The captured
