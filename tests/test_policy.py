@@ -251,3 +251,25 @@ def test_bf16_policy_rollout_within_bound_and_graph_equal():
     with pytest.raises(ValueError):
         DeviceRollout(b, agent, RunningMeanStd((66,), device="cuda"), 2, policy_dtype=torch.float16)
     b.close()
+
+
+@pytest.mark.gpu
+def test_graph_eval_matches_eager_eval():
+    """evaluate(graph=True) (one captured step replayed max_steps - 1 times) returns exactly what
+    the eager loop returns, red agents drawn from the generator included."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer.config import load_config
+    from marlsoccer.evaluate import evaluate
+    torch.manual_seed(0)
+    agent = Agent().cuda()
+    rms = RunningMeanStd(device="cuda")
+    cfg = load_config()
+    cfg["simulation"]["max_steps"] = 120
+    eager = evaluate(agent, rms, 96, seed=5, config=cfg, generator_seed=3)
+    graph = evaluate(agent, rms, 96, seed=5, config=cfg, generator_seed=3, graph=True)
+    np.testing.assert_array_equal(graph["returns"], eager["returns"])
+    np.testing.assert_array_equal(graph["score"], eager["score"])
+    assert graph["steps"] == eager["steps"] == 120
+    with pytest.raises(ValueError):
+        evaluate(agent, rms, 4, config=cfg, graph=True, frames_every=10)

@@ -5,8 +5,9 @@ at once (blue: actor mean, red: uniform random), printing per-episode returns an
 eval.py does; optionally PNG frames of episode 0.
 
     python tools/eval_batch.py --model RUN/ppo_pettingzoo_soccer.ppo_model \
-        --normalizer RUN/latest_normalizer_stats.npz [--episodes 5] [--seed S] [--png-dir DIR]
-Without --model the policy is randomly initialised (a smoke run).
+        --normalizer RUN/latest_normalizer_stats.npz [--episodes 5] [--seed S] [--png-dir DIR] [--graph]
+Without --model the policy is randomly initialised (a smoke run). --graph replays one captured
+step (evaluate(graph=True)); the wall time of the evaluation is printed last.
 """
 from __future__ import annotations
 
@@ -26,6 +27,8 @@ def main():
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--png-dir", default=None)
     ap.add_argument("--png-every", type=int, default=60)
+    ap.add_argument("--graph", action="store_true", help="evaluate(graph=True) (no PNG frames)")
+    ap.add_argument("--quiet", action="store_true", help="print only the summary lines")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -38,12 +41,18 @@ def main():
         agent.load_state_dict(torch.load(a.model, map_location="cuda", weights_only=True))
     agent.eval()
     rms = RunningMeanStd.load_npz(a.normalizer, device="cuda") if a.normalizer else RunningMeanStd(device="cuda")
-    res = evaluate(agent, rms, a.episodes, seed=a.seed, frames_every=a.png_every if a.png_dir else 0)
-    for ep in range(a.episodes):
+    import time
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = evaluate(agent, rms, a.episodes, seed=a.seed, frames_every=a.png_every if a.png_dir else 0, graph=a.graph)
+    wall = time.perf_counter() - t0
+    for ep in range(0 if a.quiet else a.episodes):
         r = res["returns"][ep]
         print(f"Episode {ep + 1}: steps={res['steps']} return agent_0={r[0]:.4f} agent_1={r[1]:.4f} "
               f"score blue={int(res['score'][ep, 0])} red={int(res['score'][ep, 1])}")
     print(f"mean return {float(np.mean(res['returns'])):.4f} over {a.episodes} episodes")
+    print(f"wall {wall:.3f} s for {a.episodes} episodes x {res['steps']} steps "
+          f"({a.episodes * res['steps'] / wall / 1e6:.3f} M env-steps/s{', graph' if a.graph else ''})")
     if a.png_dir:
         os.makedirs(a.png_dir, exist_ok=True)
         for t, imgs in res["frames"]:
