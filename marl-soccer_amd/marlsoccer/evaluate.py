@@ -33,6 +33,10 @@ def evaluate(agent: Agent, normalizer: RunningMeanStd, num_episodes: int, seed=N
     return sums; the loop body does not depend on t) as one HIP graph and replay it for the rest
     of the episode; same results as the eager loop. Not combined with frames_every (host
     rasters)."""
+    if red not in ("uniform", "zero"):
+        raise ValueError(f"red must be 'uniform' or 'zero', got {red!r}")
+    if graph and frames_every:
+        raise ValueError("evaluate(): graph=True cannot take frames (frames_every > 0)")
     batch = SoccerBatch(int(num_episodes), config=config, device=device, autoreset=False)
     try:
         dev = batch.device
@@ -48,11 +52,6 @@ def evaluate(agent: Agent, normalizer: RunningMeanStd, num_episodes: int, seed=N
         frames = []
         if frames_every:
             from .render import render_batch
-        if red not in ("uniform", "zero"):
-            raise ValueError(f"red must be 'uniform' or 'zero', got {red!r}")
-        if graph and frames_every:
-            raise ValueError("evaluate(): graph=True cannot take frames (frames_every > 0)")
-
         blue = torch.tensor(TRAINABLE, dtype=torch.int64, device=dev)  # on the device: a host index would copy per step
 
         def body():

@@ -273,3 +273,14 @@ def test_graph_eval_matches_eager_eval():
     assert graph["steps"] == eager["steps"] == 120
     with pytest.raises(ValueError):
         evaluate(agent, rms, 4, config=cfg, graph=True, frames_every=10)
+
+
+def test_evaluate_argument_errors_before_any_device_work():
+    """evaluate() rejects an unknown red policy and graph=True with frames before it creates
+    an env (so on CPU too)."""
+    from marlsoccer.evaluate import evaluate
+    agent, rms = Agent(), RunningMeanStd()
+    with pytest.raises(ValueError, match="red must be"):
+        evaluate(agent, rms, 4, red="greedy")
+    with pytest.raises(ValueError, match="graph=True cannot take frames"):
+        evaluate(agent, rms, 4, graph=True, frames_every=10)
