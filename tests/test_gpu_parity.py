@@ -435,3 +435,41 @@ def test_long_horizon_subsample_bitexact(ms):
     assert_state_equal(gpu.export_state()[sub], ref.export_state(), "end")
     assert gpu.stats()["arbiter_overflow"] == 0
     gpu.close()
+
+
+def test_obs_fallback_for_operands_outside_fast_domain_bitexact(ms):
+    """Frames whose operands fall outside the reduced-range division's domain (velocities and
+    spins below 2^-100, in the t-2 snapshot, the step-start state and the new state) take the
+    IEEE path for those lanes only; lanes of the same waves inside the domain keep the fast
+    path. Obs, rewards and state bit for bit against the fp32 oracle."""
+    n = 128
+    gpu = ms.SoccerBatch(n)
+    assert gpu.specialised
+    gpu.reset(seed=11)
+    for _ in range(3):  # leave the refilled stacks: the next steps emit t-2, t-1, t
+        gpu.step(torch.zeros((n, 4, 3), device=gpu.device))
+    st = gpu.export_state()
+    odd = np.arange(n) % 2 == 1
+    for f in ("vx", "vy", "w"):
+        st["body"][f][:, :4] = 0.0
+    st["body"]["vx"][odd, 1] = 1e-32     # below 2^-100: outside the fast domain
+    st["body"]["w"][odd, 2] = -3e-33
+    st["body"]["vy"][np.arange(n) % 4 == 2, 0] = 2e-38
+    st["snap"][odd, 0, 10 + 3] = 5e-34   # snapshot t-2: vx of agent 3
+    st["snap"][~odd, 0, 22 + 0] = 0.0
+    b = st["body"]  # snapshot t-1 is the step-start body state
+    st["snap"][:, 1] = np.concatenate([b["px"], b["py"], b["vx"][:, :4], b["vy"][:, :4], b["angle"][:, :4],
+                                       b["w"][:, :4]], axis=1)
+    assert int(st["hist_empty"].max()) == 0
+    gpu.import_state(st)
+    ref = orc.OracleBatch(n, "f32")
+    ref.import_state(st)
+    for t in range(6):
+        act = np.zeros((n, 4, 3), np.float32)
+        act[::3, 0, 0] = 0.5  # some envs move, so lanes of one wave differ
+        out = gpu.step(torch.from_numpy(act).to(gpu.device))
+        obs, rew, trunc, goal, score, bad = ref.step(act)
+        np.testing.assert_array_equal(out.obs.cpu().numpy(), obs, err_msg=f"obs t={t}")
+        np.testing.assert_array_equal(out.rew.cpu().numpy(), rew.astype(np.float32), err_msg=f"rew t={t}")
+    assert_state_equal(gpu.export_state(), ref.export_state(), "end")
+    gpu.close()
