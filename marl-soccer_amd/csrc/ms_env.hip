@@ -536,14 +536,16 @@ __device__ __forceinline__ void frame_store_at(const Params& P, const Snap& s, c
 template <bool AL>
 __device__ __forceinline__ void ring_emit(const Params& P, const Snap& s, float* __restrict__ row, int R, int slot) {
   float* d0 = row + slot * 22;
-  if (frame_inputs_in_range(P, s)) {
+  const bool fast = frame_inputs_in_range(P, s);
+  {  // every lane: the reduced-range path; out-of-domain lanes rewrite by the IEEE path (emit_three)
     float aa[6][3];
     pair_vectors<true>(s, aa);
     static_for<0, 4>([&](auto ac) __attribute__((always_inline)) {
       constexpr int A = decltype(ac)::value;
       frame_store_at<true, A>(P, s, aa, d0 + A * R * 22, AL);
     });
-  } else {
+  }
+  if (!fast) {
     float aa[6][3];
     pair_vectors<false>(s, aa);
     static_for<0, 4>([&](auto ac) __attribute__((always_inline)) {
