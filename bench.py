@@ -138,12 +138,20 @@ def regime(warmup: int, steps: int, max_steps: int) -> str:
             "spawn, later ones the full-random respawn)")
 
 
-def load_pmc_traffic():
+def regime_key(envs: int, max_steps: int, warmup: int, steps: int) -> str:
+    """Key of a timed window in profiles/pmc_step_kernel.json (tools/pmc_summary.py)."""
+    return f"e{envs}_ms{max_steps}_w{warmup}_s{steps}"
+
+
+def load_pmc_traffic(key: str):
+    """The committed rocprofv3 PMC figures of the step kernel over the same timed window
+    (dispatches warmup .. warmup + steps of a run with the same arguments), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d
+        r = d["regimes"][key]
+        return dict(r, source=f"profiles/{d['tag']}_pmc.json", tag=d["tag"])
     except Exception:
         return None
 
@@ -170,6 +178,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from marlsoccer import FrameRingBatch, SoccerBatch
+    from marlsoccer.distributed import all_gather_rows
 
     E = args.envs
     cfg = None
@@ -198,14 +207,26 @@ def main():
     launch = (batch.launcher(actions, rew, term, trunc, goal, score) if ring else
               batch.launcher(actions, obs, rew, term, trunc, goal, score))
 
+    nccl = world > 1 and dist.get_backend() == "nccl"
+
+    def gather_into(dst):
+        # RCCL all_gather_into_tensor; in the gloo rehearsal the product's all_gather_rows
+        # (device tensors staged through host memory)
+        if nccl:
+            dist.all_gather_into_tensor(dst, obs)
+        else:
+            dst.copy_(all_gather_rows(obs, world))
+
     def one(i):
         launch(i)
         if gathered is not None:
-            dist.all_gather_into_tensor(gathered, obs)
+            gather_into(gathered)
 
     for i in range(args.warmup):
         one(i)
     torch.cuda.synchronize()
+    overflow_warmup = batch.stats()["arbiter_overflow"]
+    batch.reset_stats()  # the kernel's cache-entry tally now counts the timed launches only
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -223,7 +244,7 @@ def main():
     for i in range(args.steps):
         launch(args.warmup + i)
         if gathered is not None:
-            dist.all_gather_into_tensor(gathered, obs)
+            gather_into(gathered)
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -231,6 +252,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
+    # the arbiter-cache entries the timed launches read and wrote (counted by the kernel)
+    stats = batch.stats()
 
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if shared else dev)
@@ -240,29 +263,34 @@ def main():
     # With N > 1 ranks and no --allgather: a second, shorter timed loop WITH the whole-batch
     # obs all-gather after every step (BASELINE configs[3]; SURVEY.md 8(e) asks for the rate
     # with and without it). Reported beside `value`, which stays the no-collective rate.
+    # (In the one-GPU gloo rehearsal the same loop runs through the product's all_gather_rows,
+    # staged through host memory: it exercises the path, its rate is not RCCL's.)
     gather_report = None
-    if world > 1 and gathered is None and not shared and not ring:
+    if world > 1 and gathered is None and not ring:
         gbuf = torch.empty((world * E, 4, 66), dtype=torch.float32, device=dev)
-        gk = min(200, args.steps)
+        gk = min(200 if nccl else 20, args.steps)
         for i in range(5):
             launch(i)
-            dist.all_gather_into_tensor(gbuf, obs)
+            gather_into(gbuf)
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
         g0 = time.perf_counter()
         for i in range(gk):
             launch(5 + i)
-            dist.all_gather_into_tensor(gbuf, obs)
+            gather_into(gbuf)
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
-        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
+        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev if nccl else "cpu")
         dist.all_reduce(gt, op=dist.ReduceOp.MAX)
         g_el = float(gt[0])
         gather_report = {"value": world * E * gk / g_el, "unit": "env-steps/s", "steps": gk,
                          "ms_per_step": g_el * 1e3 / gk,
-                         "collective": f"RCCL all_gather_into_tensor of obs, {E * 1056 / 1e6:.1f} MB per rank per step"}
+                         "collective": (f"RCCL all_gather_into_tensor of obs, {E * 1056 / 1e6:.1f} MB per rank per step"
+                                        if nccl else
+                                        f"gloo all_gather of obs staged through host memory (one-GPU rehearsal of "
+                                        f"the path, not RCCL's rate), {E * 1056 / 1e6:.1f} MB per rank per step")}
         del gbuf
 
     # The opt-in frame-ring layout timed beside the headline (N = 1, default run): same envs,
@@ -287,14 +315,12 @@ def main():
                        "obs": "strided (N, 4, 66) window into a (N, 4, 32, 22) frame ring, same values as obs "
                               "(bench.py --frame-ring 32 gives its roofline line)"}
 
-    # cached arbiters per env (the cache bytes of the algorithmic count), sampled mid-episode:
-    # 300 more untimed steps, so the sample is not the just-reset state at an episode boundary
-    for i in range(300):
-        launch(i)
-    torch.cuda.synchronize()
-    st = batch.export_state()
-    mean_arb = float(st["n_arb"].mean())
-    stats = batch.stats()
+    # arbiter-cache entries per env-step read and written by the timed launches themselves
+    # (the kernel's per-block tally, ms_stats): the cache term of the algorithmic byte count
+    steps_counted = max(1, stats["env_steps"])
+    arb_read = stats["cache_entries_read"] / steps_counted
+    arb_written = stats["cache_entries_written"] / steps_counted
+    mean_arb = 0.5 * (arb_read + arb_written)
     bytes_per_step = SURVEY_BYTES + 2 * ARB_BYTES * mean_arb
     layout_bytes = LAYOUT_READ + LAYOUT_WRITE + 2 * ARB_BYTES * mean_arb
     if ring:
@@ -303,21 +329,22 @@ def main():
         layout_bytes += (352 + 2 * 352 / (ring - 2)) - 1056 - 104 + 104 / (ring - 2)
     achieved = bytes_per_step * E / (kern_ms * 1e-3) / 1e9
     window = regime(args.warmup, args.steps, args.max_steps)
-    steady = window.startswith("steady state")
     value = world * E * args.steps / elapsed
     if rank == 0:
-        pmc = load_pmc_traffic()
+        key = regime_key(E, args.max_steps, args.warmup, args.steps)
+        pmc = None if ring else load_pmc_traffic(key)
         traffic = None
         pmc_info = None
-        if pmc and pmc.get("envs") == E and not ring:
-            # HBM bytes per launch from the committed rocprofv3 PMC passes (a steady-state
-            # window); divided by this run's kernel time only when this run timed the same regime
-            pmc_info = {"source": f"profiles/{pmc['tag']}_pmc.json", "bytes_per_launch": pmc["hbm_bytes_per_launch"],
-                        "regime": pmc.get("regime", "steady state (warmup 1000, 200 steps)"),
+        if pmc:
+            # HBM bytes per launch measured by rocprofv3 (FETCH_SIZE x 2 + WRITE_SIZE, separate
+            # passes) over the same dispatches of a run with these arguments, divided by this
+            # run's per-launch time
+            pmc_info = {"source": pmc["source"], "window": key, "bytes_per_launch": pmc["hbm_bytes_per_launch"],
+                        "read_bytes_per_launch": pmc["hbm_read_bytes_per_launch"],
+                        "write_bytes_per_launch": pmc["hbm_write_bytes_per_launch"],
                         "alg_bytes_per_launch": bytes_per_step * E,
                         "layout_bytes_per_launch": layout_bytes * E}
-            if steady:
-                traffic = pmc["hbm_bytes_per_launch"] / (kern_ms * 1e-3) / 1e9
+            traffic = pmc["hbm_bytes_per_launch"] / (kern_ms * 1e-3) / 1e9
         line = {
             "metric": METRIC,
             "value": value,
@@ -344,6 +371,9 @@ def main():
                           if ring else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         # the HBM bytes rocprofv3 measured (traffic) over the same time: the
+                         # fraction of peak the launch really moves
+                         "frac_measured": None if traffic is None else traffic / HBM_PEAK_GBS,
                          "kernel": "ms_step_ring_kernel" if ring else "ms_step_kernel", "kernel_ms": kern_ms,
                          "kernel_ms_method": "HIP events around the K back-to-back launches / K",
                          "alg_bytes_per_env_step": bytes_per_step,
@@ -352,14 +382,17 @@ def main():
                                               "arbiters") if ring else
                                              "SURVEY.md §8(d): 2,289 + 2 x 20 B x mean cached arbiters",
                          "layout_bytes_per_env_step": layout_bytes,
-                         "traffic_source": (pmc_info["source"] + " (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch) "
-                                            "over this run's kernel_ms") if traffic is not None else
-                                           ("not this regime: the committed PMC counters are steady-state "
-                                            "(see pmc)") if pmc_info else None,
-                         "mean_cached_arbiters": mean_arb,  # sampled mid-episode after the timed window
+                         "traffic_source": (pmc_info["source"] + f" window {key} (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE "
+                                            "per launch, same dispatches of a run with these arguments) over this "
+                                            "run's kernel_ms") if traffic is not None else
+                                           f"no committed PMC pass for window {key}",
+                         # counted by the kernel over the timed launches (ms_stats tally)
+                         "mean_cached_arbiters": mean_arb,
+                         "cache_entries_per_env_step": {"read": arb_read, "written": arb_written,
+                                                        "env_steps_counted": stats["env_steps"]},
                          "pmc": pmc_info},
             "regime": window,
-            "arbiter_overflow": stats["arbiter_overflow"],
+            "arbiter_overflow": overflow_warmup + stats["arbiter_overflow"],
         }
         if gather_report is not None:
             line["with_obs_allgather"] = gather_report

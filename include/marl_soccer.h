@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 1
+#define MS_ABI_VERSION 2
 
 #define MS_N_AGENTS 4
 #define MS_N_BODIES 5 /* 4 agents + ball */
@@ -173,6 +173,12 @@ typedef struct ms_stats {
   uint64_t arbiter_overflow;  /* arbiters dropped because MS_MAX_ARBITERS was full */
   uint64_t nonfinite_envs;    /* env-steps skipped because an action was not finite */
   int64_t first_nonfinite_env;/* lowest env index with a non-finite action, -1 if none */
+  /* Since the last ms_reset_stats, counted inside ms_step / ms_step_ring (ABI 2): env-steps
+   * taken, and the arbiter-cache entries they read (the previous step's cache) and wrote (this
+   * step's), i.e. the warm-start cache traffic of the algorithmic byte count (20 B per entry). */
+  uint64_t env_steps;
+  uint64_t cache_entries_read;
+  uint64_t cache_entries_written;
 } ms_stats;
 
 typedef struct ms_env ms_env;

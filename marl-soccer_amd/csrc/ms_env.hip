@@ -70,6 +70,7 @@ struct DevState {
   unsigned long long* stamps;  // MS_STAMPS diagnostic builds only: [wave][MS_NSTAMP] s_memtime
   char* blocks;                // [ceil(n / 64)] state blocks
   void* SP;  // contact slots KREG.. of each env (pile-ups only): [env][MAXC - KREG] CSlot
+  uint4* tally;  // [ceil(n / 64)] per-block counts since ms_reset_stats: cache entries read, written, env-steps
   int64_t n;
 };
 
@@ -798,6 +799,17 @@ __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int
   st_v(L, bb, lane, vmadd(j, mb, vb), __builtin_fmaf(ib, vcross(r2, j), wb_));
 }
 
+// Cross-lane hand-off through LDS inside one wave: every lane's LDS writes before it are
+// visible to every lane's LDS reads after it. A wave's LDS instructions execute in order, so no
+// wait is needed; the fences (wavefront scope) and the wave barrier keep the compiler and the
+// machine scheduler from moving LDS accesses across the hand-off, whatever the scheduling
+// strategy ("Faults").
+__device__ __forceinline__ void wave_lds_handoff() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // number of set bits of m below this lane
 __device__ __forceinline__ int lane_rank(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -1066,7 +1078,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
         L.u.np.nt.task[tf - base] = (uint32_t)(lane << 5) | (uint32_t)q;
         ++tf;
       }
-      asm volatile("" ::: "memory");
+      wave_lds_handoff();  // tasks posted -> read by the testing lanes
       ACC_BEGIN(sa_col);
       if (rank < total - base) {
         const uint32_t v = L.u.np.nt.task[rank];
@@ -1082,7 +1094,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
                                              __int_as_float(col.hash[1]));
       }
       ACC_END(sa_col);
-      asm volatile("" ::: "memory");
+      wave_lds_handoff();  // results written -> read by the owner lanes
       ACC_BEGIN(sa_add);
       while (mc && tc < base + nact) {
         const int q = __builtin_ctz(mc);
@@ -1103,7 +1115,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
         ACC_INC(sa_n);
       }
       ACC_END(sa_add);
-      asm volatile("" ::: "memory");
+      wave_lds_handoff();  // results read -> the next window's tasks and results overwrite them
     }
   }
   STAMP(13);
@@ -1351,6 +1363,7 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
   }
 
   float pvx[5], pvy[5];
+  int ncw = 0;  // arbiter-cache entries this step wrote
   if (active) {
     float fx[4], fy[4], tq[4];
 #pragma unroll
@@ -1374,6 +1387,7 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     unsigned long long ovf = 0;
     STAMP(1);
     physics_step(S, at, e, P, E, fx, fy, tq, L, &ovf, h2, pk0, !RING || rg.wrap != 0);
+    ncw = META_NC(E.meta);
     // positions back from LDS (written by the position phase, unchanged since)
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
@@ -1438,6 +1452,22 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     store_scalars(at, E);
   }
   STAMP(10);
+  // The wave's tally of arbiter-cache entries read (the previous step's cache) and written, and
+  // of env-steps taken: the cache term of the algorithmic byte count, measured inside the timed
+  // launches (ms_get_stats). Packed as read | written << 12 | steps << 24 (64 lanes x <= 32
+  // entries < 2^12), summed over the wave, then three no-return vector atomics by lane 0 to the
+  // block's own counters (no address is shared between waves).
+  {
+    uint32_t v = active ? ((uint32_t)nco | ((uint32_t)ncw << 12) | (1u << 24)) : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) {
+      uint4* t = S.tally + blockIdx.x;
+      atomicAdd(&t->x, v & 0xfffu);
+      atomicAdd(&t->y, (v >> 12) & 0xfffu);
+      atomicAdd(&t->z, v >> 24);
+    }
+  }
 }
 
 template <bool DEFAULT_PARAMS>
@@ -1839,12 +1869,16 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
     return fail(MS_ERR_OUT_OF_MEMORY, "stamps");
   (void)hipMemsetAsync(h->S.stamps, 0, sizeof(unsigned long long) * MS_NSTAMP * ((n + MS_BLOCK - 1) / MS_BLOCK), h->stream);
 #endif
-  if (hipMalloc((void**)&h->ctr, sizeof(Counters)) != hipSuccess) {
+  const size_t nblk = (n + BLK - 1) / BLK;
+  if (hipMalloc((void**)&h->ctr, sizeof(Counters)) != hipSuccess ||
+      hipMalloc((void**)&h->S.tally, sizeof(uint4) * nblk) != hipSuccess) {
     (void)hipFree(h->mem);
     (void)hipFree(h->S.SP);
+    (void)hipFree(h->ctr);
     delete h;
     return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of counters failed");
   }
+  HIPCHK(hipMemsetAsync(h->S.tally, 0, sizeof(uint4) * nblk, h->stream));
   HIPCHK(hipMemsetAsync(h->mem, 0, total, h->stream));
   Counters c0 = {0, 0, (long long)INT64_MAX};
   HIPCHK(hipMemcpyAsync(h->ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, h->stream));
@@ -1879,6 +1913,7 @@ int ms_destroy(ms_env* h) {
   (void)hipFree(h->mem);
   (void)hipFree(h->S.SP);
   (void)hipFree(h->ctr);
+  (void)hipFree(h->S.tally);
   delete h;
   return MS_OK;
 }
@@ -1997,6 +2032,20 @@ int ms_get_stats(ms_env* h, ms_stats* out) {
   out->arbiter_overflow = c.overflow;
   out->nonfinite_envs = c.nonfinite;
   out->first_nonfinite_env = c.first_bad == (long long)INT64_MAX ? -1 : c.first_bad;
+  const size_t nblk = (size_t)((h->n + BLK - 1) / BLK);
+  uint4* t = (uint4*)malloc(sizeof(uint4) * nblk);
+  if (!t) return fail(MS_ERR_OUT_OF_MEMORY, "ms_get_stats: host buffer");
+  if (hipMemcpy(t, h->S.tally, sizeof(uint4) * nblk, hipMemcpyDeviceToHost) != hipSuccess) {
+    free(t);
+    return fail(MS_ERR_HIP, "ms_get_stats: reading the per-block tally failed");
+  }
+  out->env_steps = out->cache_entries_read = out->cache_entries_written = 0;
+  for (size_t b = 0; b < nblk; ++b) {
+    out->cache_entries_read += t[b].x;
+    out->cache_entries_written += t[b].y;
+    out->env_steps += t[b].z;
+  }
+  free(t);
   return MS_OK;
 }
 
@@ -2012,6 +2061,9 @@ int ms_reset_stats(ms_env* h) {
   if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_reset_stats: null handle");
   Counters c0 = {0, 0, (long long)INT64_MAX};
   HIPCHK(hipMemcpyAsync(h->ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemsetAsync(h->S.tally, 0, sizeof(uint4) * (size_t)((h->n + BLK - 1) / BLK), h->stream));
+  // c0 lives on this stack frame: the copy must have read it before the call returns
+  HIPCHK(hipStreamSynchronize(h->stream));
   return MS_OK;
 }
 

@@ -41,7 +41,8 @@ class MsConfig(C.Structure):
 
 class MsStats(C.Structure):
     _fields_ = [("arbiter_overflow", C.c_uint64), ("nonfinite_envs", C.c_uint64),
-                ("first_nonfinite_env", C.c_int64)]
+                ("first_nonfinite_env", C.c_int64), ("env_steps", C.c_uint64), ("cache_entries_read", C.c_uint64),
+                ("cache_entries_written", C.c_uint64)]
 
 
 # numpy view of ms_env_state (include/marl_soccer.h), for export/import

@@ -317,7 +317,9 @@ class SoccerBatch:
         st = N.MsStats()
         N.check(self._L.ms_get_stats(self._h, C.byref(st)), "ms_get_stats")
         return {"arbiter_overflow": int(st.arbiter_overflow), "nonfinite_envs": int(st.nonfinite_envs),
-                "first_nonfinite_env": int(st.first_nonfinite_env)}
+                "first_nonfinite_env": int(st.first_nonfinite_env), "env_steps": int(st.env_steps),
+                "cache_entries_read": int(st.cache_entries_read),
+                "cache_entries_written": int(st.cache_entries_written)}
 
     def reset_stats(self) -> None:
         N.check(self._L.ms_reset_stats(self._h), "ms_reset_stats")
@@ -425,7 +427,8 @@ class FrameRingBatch(SoccerBatch):
 
     def launcher(self, actions: list, rew=None, term=None, trunc=None, goal=None, score=None):
         """Pre-bound ms_step_ring for a hot loop (SoccerBatch.launcher without obs): f(i)
-        steps with actions[i % len] and advances the window."""
+        steps with actions[i % len] and advances the window (self.pos and the self.obs view,
+        as step() does)."""
         if torch.cuda.current_device() != self.device.index:
             raise RuntimeError("launcher(): make the env's device current (torch.cuda.set_device)")
         fn, h, R, fr = self._L.ms_step_ring, self._h, self.ring, C.c_void_p(self.frames.data_ptr())
@@ -440,6 +443,7 @@ class FrameRingBatch(SoccerBatch):
             if rc:
                 N.check(rc, "ms_step_ring")
             self.pos = pos
+            self.obs = self._window(pos)
 
         step._keepalive = keep
         return step

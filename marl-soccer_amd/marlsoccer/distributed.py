@@ -64,16 +64,20 @@ def unpack_step_outputs(buf) -> dict:
 
 def all_gather_rows(buf, world: int, group=None):
     """Concatenate every rank's (n, k) tensor along dim 0 (equal n): all_gather_into_tensor on
-    RCCL, the list form on backends without it (gloo, used by the CPU tests)."""
+    RCCL, the list form on backends without it (gloo: the CPU tests and the shared-GPU
+    rehearsal, whose device tensors are staged through host memory because gloo's all_gather
+    takes CPU tensors only). The result is on buf's device."""
     import torch
     import torch.distributed as dist
     if dist.get_backend(group) == "nccl":
         dst = torch.empty((world * buf.shape[0],) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device)
         dist.all_gather_into_tensor(dst, buf, group=group)
         return dst
-    parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf, group=group)
-    return torch.cat(parts, dim=0)
+    src = buf.cpu() if buf.is_cuda else buf
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src, group=group)
+    out = torch.cat(parts, dim=0)
+    return out.to(buf.device) if buf.is_cuda else out
 
 
 class ShardedSoccerEnv:
@@ -84,11 +88,13 @@ class ShardedSoccerEnv:
     union of the shards is the single-process batch bit for bit.
 
     batch_factory(count, config, device_index, autoreset) builds the rank's batch; the default
-    is SoccerBatch on GPU local_rank (tests inject a CPU stand-in with the same interface).
+    is SoccerBatch on GPU `device` (default: local_rank, one GPU per rank; a one-GPU rehearsal
+    passes 0 so that every rank shares cuda:0). Tests inject a CPU stand-in with the same
+    interface.
     """
 
     def __init__(self, global_envs: int, config: dict | None = None, autoreset: bool = True, group=None,
-                 batch_factory=None):
+                 batch_factory=None, device: int | None = None):
         import torch.distributed as dist
 
         self.world, self.rank, self.local_rank = dist_env()
@@ -102,7 +108,7 @@ class ShardedSoccerEnv:
 
             def batch_factory(count, cfg, dev, ar):
                 return SoccerBatch(count, config=cfg, device=dev, autoreset=ar)
-        self.batch = batch_factory(self.count, config, self.local_rank, autoreset)
+        self.batch = batch_factory(self.count, config, self.local_rank if device is None else int(device), autoreset)
         self.device = self.batch.device
 
     def reset(self, seed: int | None = None, options=None):

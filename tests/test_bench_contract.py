@@ -39,4 +39,9 @@ def test_bench_prints_one_contract_line():
     assert cb["unit"] == "env-steps/s" and cb["sample"]
     assert d["arbiter_overflow"] == 0
     assert d["regime"].startswith("first episode only")  # steps 5-35 of a 1,000-step episode
-    assert rl["traffic"] is None or d["regime"].startswith("steady state")
+    # traffic only from a committed PMC pass over the same window of a run with these arguments
+    assert rl["traffic"] is None or rl["pmc"]["window"] == "e4096_ms1000_w5_s30"
+    assert rl["frac_measured"] is None or abs(rl["frac_measured"] - rl["traffic"] / rl["peak"]) < 1e-9
+    cache = rl["cache_entries_per_env_step"]
+    assert cache["env_steps_counted"] == 4096 * 30 and cache["read"] >= 0 and cache["written"] >= 0
+    assert abs(rl["mean_cached_arbiters"] - 0.5 * (cache["read"] + cache["written"])) < 1e-9

@@ -41,34 +41,53 @@ def compiler_usage(tag, kernel):
     return dict(out, source=f"profiles/{tag}_resource_usage.txt", kernel="ms_step_kernel<true> (default physics)") if out else None
 
 
-def main(tag, envs=65536, kernel="ms_step_kernel", warmup=1000, steps=1000):
+def window_pmc(src, kernel, envs, warmup, steps):
+    """HBM bytes per launch over dispatches [warmup, warmup + steps) of the step kernel in the
+    FETCH_SIZE and WRITE_SIZE passes of one bench window (medians over the window)."""
+    out = {}
+    vals = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        path = os.path.join(src, f"pmc_{c}_w{warmup}_s{steps}", "run_counter_collection.csv")
+        if not os.path.exists(path):
+            return None
+        _, rows = per_kernel(path, kernel)
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        win = rows[warmup:warmup + steps]
+        vals[c] = [float(r["Counter_Value"]) for r in win]
+        out["dispatches"] = [warmup, warmup + len(win)]
+        out["rocprof_vgpr_field"] = int(rows[0]["VGPR_Count"])
+        out["rocprof_accum_vgpr_field"] = int(rows[0]["Accum_VGPR_Count"])
+        out["sgpr"] = int(rows[0]["SGPR_Count"])
+        out["scratch_bytes_per_lane"] = int(rows[0]["Scratch_Size"])
+        out["lds_bytes_per_block"] = int(rows[0]["LDS_Block_Size"])
+    fetch_kib, write_kib = statistics.median(vals["FETCH_SIZE"]), statistics.median(vals["WRITE_SIZE"])
+    rd, wr = 2.0 * fetch_kib * 1024, write_kib * 1024
+    out.update({"FETCH_SIZE_KiB_median": fetch_kib, "WRITE_SIZE_KiB_median": write_kib,
+                "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
+                "hbm_bytes_per_env_step": (rd + wr) / envs})
+    return out
+
+
+def main(tag, envs=65536, kernel="ms_step_kernel", warmup=1000, steps=1000, max_steps=1000):
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     ks = [r for r in stats if kernel in r["Name"]][0]
-    fetch, rows = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), kernel)
-    write, _ = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"), kernel)
-    fetch_kib, write_kib = statistics.median(fetch), statistics.median(write)
-    rd = 2.0 * fetch_kib * 1024
-    wr = write_kib * 1024
     out = {
         "tag": tag, "kernel": kernel, "envs": envs,
         "kernel_avg_ns": float(ks["AverageNs"]), "kernel_calls": int(ks["Calls"]),
-        "FETCH_SIZE_KiB_median": fetch_kib, "WRITE_SIZE_KiB_median": write_kib,
-        "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
-        "hbm_bytes_per_launch": rd + wr,
-        "hbm_bytes_per_env_step": (rd + wr) / envs,
-        # rocprofv3's dispatch fields, kept verbatim: they do not match the compiler's allocation
-        # (r02re: 204 / 0 for 256 VGPRs + 150 AGPRs), so the compiler's own resource usage is
-        # attached as "compiler" and is the one DESIGN.md quotes
-        "rocprof_vgpr_field": int(rows[0]["VGPR_Count"]), "rocprof_accum_vgpr_field": int(rows[0]["Accum_VGPR_Count"]),
-        "sgpr": int(rows[0]["SGPR_Count"]), "scratch_bytes_per_lane": int(rows[0]["Scratch_Size"]),
-        "lds_bytes_per_block": int(rows[0]["LDS_Block_Size"]),
         "compiler": compiler_usage(tag, kernel),
         "correction": "read = 2 x FETCH_SIZE (gfx950 half-count, MI355X_MICROARCH.md HBM); write = WRITE_SIZE",
+        # rocprofv3's dispatch fields (vgpr/accum_vgpr) do not match the compiler's allocation on
+        # gfx950; the compiler's own resource usage is "compiler"
+        "regimes": {},
     }
+    for w, s in ((5, 20), (1000, 200)):
+        r = window_pmc(src, kernel, envs, w, s)
+        if r is not None:
+            out["regimes"][f"e{envs}_ms{max_steps}_w{w}_s{s}"] = r
     # the bench's timed window alone (its event timing covers only those launches): dispatches
     # [warmup, warmup + steps) of the step kernel in the kernel trace
     tr = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))) if kernel in r["Kernel_Name"]]
