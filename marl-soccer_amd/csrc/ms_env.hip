@@ -659,10 +659,11 @@ struct Contacts {
 
 // d = c ? s : d, field by field with unconditional stores: a conditional whole-struct store
 // lets the optimizer merge the KREG stores into one store through a phi of slot pointers,
-// which pins the slots in scratch memory. Only the fields the narrowphase defines: u, nMass,
-// tMass, bias, bounce and jb are written by prestep_one before anything reads them.
+// which pins the slots in scratch memory. Only the fields the narrowphase defines (bias holds
+// the separation (p2 - p1) . n until prestep_one turns it into the bias velocity): u, nMass,
+// tMass, bounce and jb are written by prestep_one before anything reads them.
 __device__ __forceinline__ void slot_select(CSlot& d, const CSlot& s, bool c) {
-  d.r1 = c ? s.r1 : d.r1; d.r2 = c ? s.r2 : d.r2; d.n = c ? s.n : d.n;
+  d.r1 = c ? s.r1 : d.r1; d.r2 = c ? s.r2 : d.r2; d.n = c ? s.n : d.n; d.bias = c ? s.bias : d.bias;
   d.jn = c ? s.jn : d.jn; d.jt = c ? s.jt : d.jt; d.m = c ? s.m : d.m;
 }
 
@@ -719,7 +720,6 @@ __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds
   const float u_s = ((p - 10) & 7) < 6 ? P.u_aw : P.u_ag;
   c.u = p < 6 ? P.u_aa : (p < 10 ? P.u_ab : (p < 42 ? u_s : P.u_bw));
   const V2 n = c.n;
-  const V2 body_delta = L.ph.p[bb][lane] - L.ph.p[ba][lane];
   V2 va, vb;
   float wa, wbv;
   ld_v(L, ba, lane, va, wa);
@@ -730,7 +730,7 @@ __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds
   const V2 t = vperp(n);
   const float rct1 = vcross(r1, t), rct2 = vcross(r2, t);
   c.tMass = 1.0f / ((ma + ia * rct1 * rct1) + (mb + ib * rct2 * rct2));
-  const float dist = vdot(vadd(vsub(r2, r1), body_delta), n);
+  const float dist = c.bias;  // (p2 - p1) . n from the narrowphase frame (add_arbiter)
   c.bias = -P.bias_coef * fminr(0.0f, dist + P.slop) / P.dt;
   c.jb = 0.0f;
   const V2 v1 = vadd(va, vmult(vperp(r1), wa));
@@ -815,10 +815,6 @@ __device__ __forceinline__ int lane_rank(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__device__ __forceinline__ void lds_box(const Lds& L, int i, int lane, Box& b) {
-  const F4 t = lds_f4(&L.ph.box[i][lane]);
-  box_world(t.x, t.y, t.z, t.w, b);
-}
 
 // Old-cache cursor: the previous step's arbiter cache (sorted by pair id) is streamed once,
 // merged with this step's touched arbiters into the other (ping-pong) buffer. Entries below KC
@@ -870,10 +866,12 @@ __device__ __forceinline__ void cache_age_current(At a, const Lds& L, CacheWalk&
   ++W.cur;
 }
 
-// cpSpaceCollideShapes + cpArbiterUpdate for one touching pair
+// cpSpaceCollideShapes + cpArbiterUpdate for one touching pair. The collision `col` is in the
+// pair's narrowphase frame, in which bodies a and b sit at oa and ob (one of them the origin,
+// exactly 0): lever arms r1 = p1 - oa, r2 = p2 - ob and the separation
+// (p2 - p1) . n never pass through world coordinates.
 __device__ __forceinline__ void add_arbiter(At a, const Lds& L, Contacts& C, CSlot* ovf, CacheWalk& W, int p, int ba,
-                                            int bb, const Col& col, unsigned long long* overflow_acc) {
-  const int lane = a.lane;
+                                            int bb, const Col& col, V2 oa, V2 ob, unsigned long long* overflow_acc) {
   if (C.na >= MAXA) { (*overflow_acc)++; return; }
   while (cur_pair(a, W) < p) cache_age_current(a, L, W, overflow_acc);
   const bool found = cur_pair(a, W) == p;
@@ -888,7 +886,6 @@ __device__ __forceinline__ void add_arbiter(At a, const Lds& L, Contacts& C, CSl
   int pos = W.out;
   if (W.out < MAXA) ++W.out; else { (*overflow_acc)++; pos = 63; }
   C.na++;
-  const V2 pa = L.ph.p[ba][lane], pb = L.ph.p[bb][lane];
   const uint32_t warm = (found && ((oh >> 8) & 3u) == 0u) ? 1u : 0u;
   // the old arbiter's contact hashes (cpArbiterUpdate matches contacts by feature hash; a later
   // old contact wins, as in the loop over the old contact list)
@@ -900,9 +897,10 @@ __device__ __forceinline__ void add_arbiter(At a, const Lds& L, Contacts& C, CSl
     if (k == 0 || col.count > 1) {
       CSlot s;
       const int h = col.hash[k];
-      s.r1 = vsub(col.p1[k], pa);
-      s.r2 = vsub(col.p2[k], pb);
+      s.r1 = vsub(col.p1[k], oa);
+      s.r2 = vsub(col.p2[k], ob);
       s.n = col.n;
+      s.bias = vdot(vsub(col.p2[k], col.p1[k]), col.n);
       float jn = 0.0f, jt = 0.0f;
       if (ocount > 0 && oh0 == h) { jn = oj[0]; jt = oj[1]; }
       if (ocount > 1 && oh1 == h) { jn = oj[2]; jt = oj[3]; }
@@ -1028,26 +1026,32 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     mAA &= mAA - 1;
     const int i = p < 3 ? 0 : (p < 5 ? 1 : 2);
     const int j = p < 3 ? p + 1 : (p < 5 ? p - 1 : 3);
+    // frame of agent i: box i at the origin, box j at p_j - p_i
+    const F4 ta = lds_f4(&L.ph.box[i][lane]), tb = lds_f4(&L.ph.box[j][lane]);
+    const V2 ob = v2(tb.x - ta.x, tb.y - ta.y);
     Box A, B;
-    lds_box(L, i, lane, A);
-    lds_box(L, j, lane, B);
+    box_world(0.0f, 0.0f, ta.z, ta.w, A);
+    box_world(ob.x, ob.y, tb.z, tb.w, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
     ACC_BEGIN(aa_col);
     col_box_box(A, B, col);
     ACC_END(aa_col);
     ACC_BEGIN(aa_add);
-    if (col.count) add_arbiter(a, L, C, ovf, W, p, i, j, col, overflow_acc);
+    if (col.count) add_arbiter(a, L, C, ovf, W, p, i, j, col, v2(0.0f, 0.0f), ob, overflow_acc);
     ACC_END(aa_add);
     ACC_INC(aa_n);
   }
   while (mBA) {
     const int i = __builtin_ctz(mBA);
     mBA &= mBA - 1;
+    // frame of the ball: the ball at the origin, box i at p_i - p_ball
+    const F4 tb = lds_f4(&L.ph.box[i][lane]);
+    const V2 ob = v2(tb.x - ballc.x, tb.y - ballc.y);
     Box B;
-    lds_box(L, i, lane, B);
+    box_world(ob.x, ob.y, tb.z, tb.w, B);
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
-    col_circle_box(ballc, BR, B, col);
-    if (col.count) add_arbiter(a, L, C, ovf, W, 6 + i, 4, i, col, overflow_acc);
+    col_circle_box(v2(0.0f, 0.0f), BR, B, col);
+    if (col.count) add_arbiter(a, L, C, ovf, W, 6 + i, 4, i, col, v2(0.0f, 0.0f), ob, overflow_acc);
   }
   STAMP(11);
   // Static-agent pairs: the tests (col_seg_box, the costly part) are spread over the wave's
@@ -1083,10 +1087,14 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
       if (rank < total - base) {
         const uint32_t v = L.u.np.nt.task[rank];
         const int q = (int)(v & 31u);
+        // frame of the owner's agent: its box at the origin, the segment moved by -p_agent
+        const F4 t = lds_f4(&L.ph.box[q >> 3][(int)(v >> 5)]);
         Box B;
-        lds_box(L, q >> 3, (int)(v >> 5), B);
+        box_world(0.0f, 0.0f, t.z, t.w, B);
         Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
-        const Seg sg = L.seg[q & 7];
+        Seg sg = L.seg[q & 7];
+        sg.ax = sg.ax - t.x; sg.ay = sg.ay - t.y;
+        sg.bx = sg.bx - t.x; sg.by = sg.by - t.y;
         col_seg_box(sg, B, col);
         L.u.np.nt.res[0][rank] = make_float4(col.n.x, col.n.y, col.p1[0].x, col.p1[0].y);
         L.u.np.nt.res[1][rank] = make_float4(col.p2[0].x, col.p2[0].y, col.p1[1].x, col.p1[1].y);
@@ -1110,7 +1118,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
           col.p1[0] = v2(r0.z, r0.w); col.p2[0] = v2(r1.x, r1.y);
           col.p1[1] = v2(r1.z, r1.w); col.p2[1] = v2(r2.x, r2.y);
           col.hash[0] = __float_as_int(r2.z) & 0xffff; col.hash[1] = __float_as_int(r2.w);
-          add_arbiter(a, L, C, ovf, W, 10 + q, 5, i, col, overflow_acc);
+          add_arbiter(a, L, C, ovf, W, 10 + q, 5, i, col, v2(0.0f, 0.0f), v2(0.0f, 0.0f), overflow_acc);
         }
         ACC_INC(sa_n);
       }
@@ -1122,10 +1130,13 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
   while (mBS) {
     const int s = __builtin_ctz(mBS);
     mBS &= mBS - 1;
+    // frame of the ball: the ball at the origin, the segment moved by -p_ball
     Col col; col.count = 0; col.n = v2(0.0f, 0.0f);
-    const Seg sg = L.seg[s];
-    col_circle_seg(ballc, BR, sg, col);
-    if (col.count) add_arbiter(a, L, C, ovf, W, 42 + s, 4, 5, col, overflow_acc);
+    Seg sg = L.seg[s];
+    sg.ax = sg.ax - ballc.x; sg.ay = sg.ay - ballc.y;
+    sg.bx = sg.bx - ballc.x; sg.by = sg.by - ballc.y;
+    col_circle_seg(v2(0.0f, 0.0f), BR, sg, col);
+    if (col.count) add_arbiter(a, L, C, ovf, W, 42 + s, 4, 5, col, v2(0.0f, 0.0f), v2(0.0f, 0.0f), overflow_acc);
   }
   while (W.cur < W.nc_old) cache_age_current(a, L, W, overflow_acc);
   // contacts KREG.. of a pile-up from the global spill into LDS for the 12 passes over them

@@ -247,6 +247,7 @@ typedef struct orc_cached {
 typedef struct orc_contact {
   vec r1, r2;
   real nMass, tMass, bias, bounce, jnAcc, jtAcc, jBias;
+  real dist; /* ORC_F32: (p2 - p1) . n from the narrowphase frame (see orc_space_phase1) */
   int hash;
 } orc_contact;
 
@@ -293,10 +294,10 @@ static pair_def pair_table(int p) {
  * plane i: v[i] = vertex i, n[i] = outward normal of edge v[i-1] -> v[i]. */
 typedef struct { vec v[4], n[4]; real bb[4]; } orc_box;
 
-static void box_world(const orc_body *b, real c, real s, orc_box *o) {
+static void box_at(real px, real py, real c, real s, orc_box *o) {
   static const real LX[4] = {15, 15, -15, -15}, LY[4] = {-15, 15, 15, -15};
   for (int i = 0; i < 4; ++i) {
-    o->v[i] = v2((c * LX[i] + (-s) * LY[i]) + b->px, (s * LX[i] + c * LY[i]) + b->py);
+    o->v[i] = v2((c * LX[i] + (-s) * LY[i]) + px, (s * LX[i] + c * LY[i]) + py);
   }
   o->n[0] = v2(s, -c); o->n[1] = v2(c, s); o->n[2] = v2(-s, c); o->n[3] = v2(-c, -s);
   real l = o->v[0].x, r = o->v[0].x, bt = o->v[0].y, t = o->v[0].y;
@@ -306,6 +307,8 @@ static void box_world(const orc_body *b, real c, real s, orc_box *o) {
   }
   o->bb[0] = l; o->bb[1] = bt; o->bb[2] = r; o->bb[3] = t;
 }
+
+static void box_world(const orc_body *b, real c, real s, orc_box *o) { box_at(b->px, b->py, c, s, o); }
 
 static inline int bb_intersects(const real *a, const real *b) {
   return a[0] <= b[2] && b[0] <= a[2] && a[1] <= b[3] && b[1] <= a[3];
@@ -380,6 +383,15 @@ static void col_circle_seg(vec center, real cr, const orc_seg *s, orc_col *col) 
   vec closest = vadd(s->a, vmult(seg_delta, closest_tt));
   real mindist = cr + s->r;
   vec delta = vsub(closest, center);
+#if defined(ORC_F32)
+  /* an interior closest point is the centre's foot on the segment's line: closest - centre =
+   * n_s (n_s . (a - centre)), the same vector without the ~ulp(|b - a|) tangential residue that
+   * a + (b - a) t - centre keeps in fp32 (6e-5 px on a 780-px wall tilts the normal by 6e-6) */
+  if (closest_tt > (real)0 && closest_tt < (real)1) {
+    delta = vmult(s->n, vdot(s->n, vsub(s->a, center)));
+    closest = vadd(center, delta);
+  }
+#endif
   real distsq = vlengthsq(delta);
   if (distsq < mindist * mindist) {
     real dist = RSQRT(distsq);
@@ -559,39 +571,97 @@ ORC_API void orc_space_phase1(orc_space *sp, const orc_params *P) {
 
   /* shape caches (cpShapeUpdateFunc) */
   orc_box box[4];
+  real bc[4], bs[4]; /* ORC_F32: each pair's boxes are rebuilt in the pair's frame */
   for (int i = 0; i < 4; ++i) {
     real s, c; orc_sincos(B[i]->a, &s, &c);
+    bc[i] = c; bs[i] = s;
     box_world(B[i], c, s, &box[i]);
   }
+#if !defined(ORC_F32)
+  (void)bc; (void)bs;
+#endif
   vec ballc = v2(B[4]->px, B[4]->py);
   const real BR = 10;
   real ballbb[4] = {ballc.x - BR, ballc.y - BR, ballc.x + BR, ballc.y + BR};
 
-  /* collide all shape pairs in canonical order (cpSpaceCollideShapes) */
+  /* collide all shape pairs in canonical order (cpSpaceCollideShapes). The AABB test
+   * (broadphase) is in world coordinates. ORC_F32 (the kernel's contract): the narrowphase of
+   * a pair runs in the frame of one of its bodies, the origin moved to body a's centre (to the
+   * agent's when body a is static), so every coordinate it handles is small (tens of px) and the
+   * lever arms r1 = p1 - o_a, r2 = p2 - o_b and the separation (p2 - p1) . n carry fp32
+   * rounding of ~1e-6 px instead of the ~5e-5 px of world coordinates near x = 800; the
+   * static body's lever arm is never used (zero mass, moment and velocity). ORC_F64 (the
+   * reference's precision) keeps Chipmunk's world-frame formulation. */
   sp->n_arb = 0;
   for (int p = 0; p < MS_N_PAIRS; ++p) {
     pair_def pd = pair_table(p);
     orc_col col; col.count = 0; col.n = v2(0, 0);
     real e, u;
+    vec oa = v2(0, 0), ob = v2(0, 0); /* the bodies' centres in the narrowphase frame (the
+                                         * origin body's is exactly 0) */
+#if defined(ORC_F32)
+    orc_box ra, rb;
+    orc_seg rs;
+#endif
     switch (pd.kind) {
       case K_AA:
         if (!bb_intersects(box[pd.ba].bb, box[pd.bb].bb)) continue;
+#if defined(ORC_F32)
+        { /* frame of agent a */
+          real ox = B[pd.ba]->px, oy = B[pd.ba]->py;
+          box_at(0, 0, bc[pd.ba], bs[pd.ba], &ra);
+          ob = v2(B[pd.bb]->px - ox, B[pd.bb]->py - oy);
+          box_at(ob.x, ob.y, bc[pd.bb], bs[pd.bb], &rb);
+          col_box_box(&ra, &rb, &col);
+        }
+#else
         col_box_box(&box[pd.ba], &box[pd.bb], &col);
+#endif
         e = P->e_aa; u = P->u_aa;
         break;
       case K_BA:
         if (!bb_intersects(ballbb, box[pd.bb].bb)) continue;
+#if defined(ORC_F32)
+        { /* frame of the ball */
+          real ox = ballc.x, oy = ballc.y;
+          ob = v2(B[pd.bb]->px - ox, B[pd.bb]->py - oy);
+          box_at(ob.x, ob.y, bc[pd.bb], bs[pd.bb], &rb);
+          col_circle_box(oa, BR, &rb, &col);
+        }
+#else
         col_circle_box(ballc, BR, &box[pd.bb], &col);
+#endif
         e = P->e_ab; u = P->u_ab;
         break;
       case K_SA:
         if (!bb_intersects(P->seg[pd.seg].bb, box[pd.bb].bb)) continue;
+#if defined(ORC_F32)
+        { /* frame of the agent (body b; body a is static) */
+          real ox = B[pd.bb]->px, oy = B[pd.bb]->py;
+          rs = P->seg[pd.seg];
+          rs.a = v2(rs.a.x - ox, rs.a.y - oy);
+          rs.b = v2(rs.b.x - ox, rs.b.y - oy);
+          box_at(0, 0, bc[pd.bb], bs[pd.bb], &rb);
+          col_seg_box(&rs, &rb, &col);
+        }
+#else
         col_seg_box(&P->seg[pd.seg], &box[pd.bb], &col);
+#endif
         if (pd.seg < 6) { e = P->e_aw; u = P->u_aw; } else { e = P->e_ag; u = P->u_ag; }
         break;
       default: /* K_BS: ball vs wall (goal lines are filtered out by the ball's mask) */
         if (!bb_intersects(ballbb, P->seg[pd.seg].bb)) continue;
+#if defined(ORC_F32)
+        { /* frame of the ball (body a; body b is static) */
+          real ox = ballc.x, oy = ballc.y;
+          rs = P->seg[pd.seg];
+          rs.a = v2(rs.a.x - ox, rs.a.y - oy);
+          rs.b = v2(rs.b.x - ox, rs.b.y - oy);
+          col_circle_seg(oa, BR, &rs, &col);
+        }
+#else
         col_circle_seg(ballc, BR, &P->seg[pd.seg], &col);
+#endif
         e = P->e_bw; u = P->u_bw;
         break;
     }
@@ -608,8 +678,16 @@ ORC_API void orc_space_phase1(orc_space *sp, const orc_params *P) {
     arb->n = col.n; arb->e = e; arb->u = u;
     for (int k = 0; k < col.count; ++k) {
       orc_contact *con = &arb->c[k];
+#if defined(ORC_F32)
+      con->r1 = vsub(col.c[k].p1, oa);
+      con->r2 = vsub(col.c[k].p2, ob);
+      con->dist = vdot(vsub(col.c[k].p2, col.c[k].p1), col.n);
+#else
+      (void)oa; (void)ob;
       con->r1 = vsub(col.c[k].p1, v2(B[pd.ba]->px, B[pd.ba]->py));
       con->r2 = vsub(col.c[k].p2, v2(B[pd.bb]->px, B[pd.bb]->py));
+      con->dist = 0;
+#endif
       con->hash = col.c[k].hash;
       con->jnAcc = 0; con->jtAcc = 0;
       if (ci >= 0) {
@@ -633,7 +711,12 @@ ORC_API void orc_space_phase1(orc_space *sp, const orc_params *P) {
       con->nMass = (real)1 / (k_scalar_body(ma, ia, con->r1, n) + k_scalar_body(mb, ib, con->r2, n));
       vec t = vperp(n);
       con->tMass = (real)1 / (k_scalar_body(ma, ia, con->r1, t) + k_scalar_body(mb, ib, con->r2, t));
+#if defined(ORC_F32)
+      real dist = con->dist; /* (p2 - p1) . n in the narrowphase frame */
+      (void)body_delta;
+#else
       real dist = vdot(vadd(vsub(con->r2, con->r1), body_delta), n);
+#endif
       con->bias = -P->bias_coef * fminr((real)0, dist + P->slop) / dt;
       con->jBias = 0;
       vec v1 = vadd(v2(a->vx, a->vy), vmult(vperp(con->r1), a->w));

@@ -83,30 +83,72 @@ def step_errors(st32, st64, obs32, obs64, rew32, rew64) -> dict:
     return out
 
 
-# The bars. Positions, angles, position-derived observations and rewards: 1e-5 at every state.
-# Velocities: 1e-5 at 95 % of states; the rest are mostly squeeze states (the ball, mass 1, wedged
-# between an agent, mass 10, and a wall, or two agents pressed together), where the contact
-# impulses are hundreds of times the resulting velocity change and the 10-iteration
-# Gauss-Seidel solve (cpSpace iterations = 10) passes fp32's rounding of the lever arms and
-# normals (about 3e-5 px at 400 px) through impulses of ~500 to the angular velocity; there the
-# error is bounded by VEL_MAX.
-VEL_Q = 0.95
-VEL_MAX = 5e-4
-EXACT_BARS = ("px", "py", "angle", "obs_pos", "obs_angle", "rew")
-VEL_BARS = ("vx", "vy", "w", "vbx", "vby", "wb", "obs_vel")
+# The bars. Every quantity within 1e-5 at every state, except the angular velocity (and the
+# observation component built from it, obs_vel), which is held to a per-state bound set by
+# the reference's own conditioning at that state: max(1e-5, COND_FACTOR x the largest change
+# of the f64 step's result when ONE fp32 input of the state (a position, velocity, angle or
+# spin of one body) moves by one ulp). The fp32 env cannot know the reference's state better
+# than half an ulp of each stored float, so where one ulp of input moves the f64 answer by more
+# than 1e-5 no fp32 implementation can promise 1e-5: those are squeeze states (the ball, mass
+# 1, wedged between an agent and a wall, or agents pressed together), where normal impulses of
+# ~2,000 meet a 10-iteration Gauss-Seidel solve. 59 of the 9,420 states are such states; at all
+# of them the fp32 error is within 1.2x of that one-ulp sensitivity.
+EXACT_BARS = ("px", "py", "angle", "obs_pos", "obs_angle", "rew", "vx", "vy", "vbx", "vby", "wb")
+COND_BARS = ("w", "obs_vel")
+COND_FACTOR = 2.0
+_AGENT_FIELDS = ("px", "py", "vx", "vy", "angle", "w")
+_BALL_FIELDS = ("px", "py", "vx", "vy", "w")
+PERTURBATIONS = tuple((b, f, d) for b in range(4) for f in _AGENT_FIELDS for d in (1, -1)) + \
+    tuple((4, f, d) for f in _BALL_FIELDS for d in (1, -1))
 
 
-def check_one_step(errs: dict, where: str = "") -> dict:
-    """Assert the bars; return a summary {quantity: (max, q99)}."""
+@functools.lru_cache(maxsize=None)
+def conditioning(name: str, chunk: int = 1000) -> dict:
+    """Per state of trajectory `name`: for every quantity of step_errors, the largest change of
+    the f64 oracle's one-step result over PERTURBATIONS (one fp32 input field of one body moved
+    one ulp up or down), in step_errors' units. {quantity: (n,) array}."""
+    states, actions, cfg = fixture_states(name)
+    n, k = len(states), len(PERTURBATIONS)
+    out = {}
+    for c0 in range(0, n, chunk):
+        st, ac = states[c0:c0 + chunk], actions[c0:c0 + chunk]
+        m = len(st)
+        b64, bo, br, _ = oracle_one_step(st, ac, cfg, "f64")
+        big = np.repeat(st[None], k, 0)
+        for j, (b, f, d) in enumerate(PERTURBATIONS):
+            x = big[j]["body"][f][:, b].astype(np.float32)
+            big[j]["body"][f][:, b] = np.nextafter(x, np.float32(d * np.inf))
+        p64, po, pr, _ = oracle_one_step(big.reshape(-1), np.tile(ac, (k, 1, 1)), cfg, "f64")
+        e = step_errors(p64, np.tile(b64, k), po, np.tile(np.asarray(bo), (k, 1, 1)), pr, np.tile(np.asarray(br), (k, 1)))
+        for q, v in e.items():
+            out.setdefault(q, np.zeros(n))[c0:c0 + m] = v.reshape(k, m).max(axis=0)
+    return out
+
+
+def check_one_step(errs: dict, cond: dict, where: str = "") -> dict:
+    """Assert the bars (cond: conditioning() of the same states); return a summary
+    {quantity: (max error, states held to the conditioned bound)}."""
     summary = {}
-    for k, e in errs.items():
-        summary[k] = (float(e.max()), float(np.quantile(e, VEL_Q)))
     for k in EXACT_BARS:
-        assert summary[k][0] <= TOL, f"{where} {k}: max error {summary[k][0]:.3e} > {TOL}"
-    for k in VEL_BARS:
-        assert summary[k][1] <= TOL, f"{where} {k}: {VEL_Q:.0%} quantile {summary[k][1]:.3e} > {TOL}"
-        assert summary[k][0] <= VEL_MAX, f"{where} {k}: max error {summary[k][0]:.3e} > {VEL_MAX}"
+        mx = float(errs[k].max())
+        summary[k] = (mx, 0)
+        assert mx <= TOL, f"{where} {k}: max error {mx:.3e} > {TOL}"
+    for k in COND_BARS:
+        bound = np.maximum(TOL, COND_FACTOR * cond[k])
+        bad = np.flatnonzero(errs[k] > bound)
+        summary[k] = (float(errs[k].max()), int((errs[k] > TOL).sum()))
+        assert bad.size == 0, (f"{where} {k}: state {bad[0]} error {errs[k][bad[0]]:.3e} > max(1e-5, "
+                               f"{COND_FACTOR} x one-ulp sensitivity {cond[k][bad[0]]:.3e})")
     return summary
+
+
+# Horizons from identical states (1-120 steps): the first step at which a quantity leaves 1e-5
+# is set by the first ill-conditioned state on the way (a squeezed ball a few steps in makes w
+# leave the bound, and the trajectories then part ways chaotically), so it changes with any
+# change of fp32 rounding; the table is in DESIGN.md §4. The bars: positions and rewards stay
+# within 1e-5 for more than 20 steps from every start, angles for more than 15, the
+# position-derived observations for more than 10.
+HORIZON_BARS = {"px": 20, "py": 20, "angle": 15, "rew": 20, "obs_pos": 10}
 
 
 def flags_equal(a, b, where=""):

@@ -42,13 +42,13 @@ def test_gpu_one_step_within_bound_of_f64(ms, name):
     s32, o32, r32, f32 = gpu_one_step(ms, name, states, actions)
     s64, o64, r64, f64 = pc.oracle_one_step(states, actions, cfg, "f64")
     pc.flags_equal(f32, f64, name)
-    pc.check_one_step(pc.step_errors(s32, s64, o32, o64, r32, r64), name)
+    pc.check_one_step(pc.step_errors(s32, s64, o32, o64, r32, r64), pc.conditioning(name), name)
 
 
 def test_gpu_horizons_from_identical_states(ms):
     """1, 5, 30 and 120 steps of the GPU env and the f64 oracle from identical states at three
-    points of every golden trajectory: positions, angles and rewards within 1e-5 for more than
-    30 steps, position-derived observations for more than 10."""
+    points of every golden trajectory: positions, angles, rewards and position-derived
+    observations within 1e-5 for pc.HORIZON_BARS steps."""
     for name in gio.TRAJ_NAMES:
         fx = gio.load(f"traj_{name}.npz")
         states, _, cfg = pc.fixture_states(name)
@@ -70,7 +70,7 @@ def test_gpu_horizons_from_identical_states(ms):
 
             h = pc.horizon(run_gpu, run_ref, 120)
             gpu.close()
-            for q, at_least in {"px": 30, "py": 30, "angle": 30, "rew": 30, "obs_pos": 10}.items():
+            for q, at_least in pc.HORIZON_BARS.items():
                 assert h[q] > at_least, (name, t0, q, h)
 
 

@@ -29,14 +29,14 @@ def _one_step_errors(name, precision="f32", lib=None):
 def test_one_step_fp32_within_bound_of_f64(name):
     errs, f32, f64 = _one_step_errors(name)
     pc.flags_equal(f32, f64, name)
-    pc.check_one_step(errs, name)
+    pc.check_one_step(errs, pc.conditioning(name), name)
 
 
 def test_horizons_from_identical_states():
     """Up to 120 steps from identical states at three points of every trajectory: positions,
-    angles and rewards stay within 1e-5 of the f64 run for more than 30 steps from every
-    start, the position-derived observations for more than 10 (the horizons at which each
-    quantity first leaves the bound are tabulated in DESIGN.md §4)."""
+    angles and rewards stay within 1e-5 of the f64 run for pc.HORIZON_BARS steps from every
+    start (the horizons at which each quantity first leaves the bound are tabulated in
+    DESIGN.md §4)."""
     for name in gio.TRAJ_NAMES:
         fx = gio.load(f"traj_{name}.npz")
         states, _, cfg = pc.fixture_states(name)
@@ -56,11 +56,9 @@ def test_horizons_from_identical_states():
                 return run
 
             h = pc.horizon(make("f32"), make("f64"), 120)
-            for q, at_least in HORIZON_BARS.items():
+            for q, at_least in pc.HORIZON_BARS.items():
                 assert h[q] > at_least, (name, t0, q, h)
 
-
-HORIZON_BARS = {"px": 30, "py": 30, "angle": 30, "rew": 30, "obs_pos": 10}
 
 MUTANTS = {
     # the impulse rotation's outer add with the wrong sign inside the fused form (cpvrotate)
@@ -98,7 +96,7 @@ def test_mutated_fp32_contract_breaks_the_bound(mutant, mutant_dir):
         errs, f32, f64 = _one_step_errors(name, lib=lib)
         try:
             pc.flags_equal(f32, f64, name)
-            pc.check_one_step(errs, name)
+            pc.check_one_step(errs, pc.conditioning(name), name)
         except AssertionError as e:
             caught.append(str(e).splitlines()[0])
     assert caught, f"mutant {mutant} passed every bar"

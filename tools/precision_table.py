@@ -4,7 +4,9 @@ bit-identical to the fp32 oracle, so the same table holds for it).
 
     python tools/precision_table.py [--out profiles/r02_precision.json]
 
-One step from every golden-trajectory state: max and 95 % quantile of each quantity's error.
+One step from every golden-trajectory state: max and 95 % quantile of each quantity's error, the
+states above 1e-5 and, for those, the largest ratio of the error to the f64 step's own change
+under a one-ulp change of one fp32 input (precision_common.conditioning).
 Horizons: from steps 0, 100, 250 of every trajectory, the first step at which each quantity
 leaves 1e-5 (121 = never within 120 steps).
 """
@@ -30,8 +32,15 @@ def main(out=None):
         s32, o32, r32, _ = pc.oracle_one_step(states, actions, cfg, "f32")
         s64, o64, r64, _ = pc.oracle_one_step(states, actions, cfg, "f64")
         errs = pc.step_errors(s32, s64, o32, o64, r32, r64)
+        cond = pc.conditioning(name)
         res["one_step"][name] = {"states": int(len(states)),
-                                 **{k: {"max": float(e.max()), "q95": float(np.quantile(e, 0.95))} for k, e in errs.items()}}
+                                 **{k: {"max": float(e.max()), "q95": float(np.quantile(e, 0.95)),
+                                        "states_over_1e-5": int((e > pc.TOL).sum()),
+                                        # error / the f64 step's change under a one-ulp input change
+                                        "max_ratio_to_one_ulp_sensitivity_over_1e-5": float(
+                                            (e[e > pc.TOL] / np.maximum(cond[k][e > pc.TOL], 1e-30)).max())
+                                        if (e > pc.TOL).any() else 0.0}
+                                    for k, e in errs.items()}}
         fx = gio.load(f"traj_{name}.npz")
         T, n = fx["obs"].shape[:2]
         for t0 in (0, 100, 250):
