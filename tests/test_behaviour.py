@@ -172,19 +172,27 @@ def test_own_goal_is_conceded_and_penalised():
 
 
 def test_random_play_returns_match_reference_scale():
-    """Notebook cell 0 (marl-soccer.ipynb JSON L13-27): 5 random-action episodes with
-    full-random spawns score 0-0 with small positive/negative blue returns (0.15-1.28)."""
-    env = make_env()
+    """Notebook cell 0 (marl-soccer.ipynb JSON L13-27): random-action episodes with
+    full-random spawns score 0-0 with small blue returns (five episodes: 0.15-1.28). One
+    episode's return is chaotic (a single early rounding difference decides whether some agent
+    happens to kick the ball toward a goal), so the check is on the distribution of 256 such
+    episodes (seeds 100..355, uniform(-1, 1) actions, one whole 1,000-step episode each):
+    the reference's own precision (the f64 oracle, same seeds and actions) gives median 0.36,
+    |return| > 5 in 34 of 256 (a ball kicked 50+ px toward or away from the red goal: 0.1 per
+    px), no goals; the fp32 oracle (this kernel's contract) median 0.35, 32 of 256, one goal."""
+    from marlsoccer import SoccerBatch
+    n = 256
+    env = SoccerBatch(n)
+    env.reset(seed=100, options={"use_full_random_positions": True})
     rng = np.random.default_rng(0)
-    rets = []
-    for ep in range(5):
-        env.reset(seed=100 + ep, options={"use_full_random_positions": True})
-        ret, goals = 0.0, 0
-        while env.agents:
-            acts = {a: rng.uniform(-1, 1, 3).astype(np.float32) for a in env.agents}
-            _, rew, _, _, info = env.step(acts)
-            ret += rew["agent_0"]
-            goals += "goal_scored_by" in info["agent_0"]
-        rets.append(ret)
-    assert all(abs(r) < 5.0 for r in rets), rets
+    ret = np.zeros(n)
+    goals = np.zeros(n, np.int64)
+    for t in range(1000):
+        out = env.step(torch.from_numpy(rng.uniform(-1, 1, (n, 4, 3)).astype(np.float32)).to(env.device))
+        ret += out.rew[:, 0].double().cpu().numpy()
+        goals += (out.goal.cpu().numpy() != 0)
+    assert bool(out.trunc.all())
+    assert -1.0 < np.median(ret) < 1.5, np.median(ret)
+    assert (np.abs(ret) > 5.0).mean() < 0.25, np.sort(ret)
+    assert (goals == 0).mean() > 0.9 and np.abs(ret).max() < 40.0, (goals.max(), np.abs(ret).max())
     env.close()
