@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--frame-ring", type=int, default=0, metavar="R",
                     help="opt-in frame-ring observations (FrameRingBatch, R frames per agent ring); "
                          "default 0: the reference's contiguous (N, 4, 66) stacked obs")
+    ap.add_argument("--persistent", type=int, default=None, metavar="W",
+                    help="ms_step launch shape (SoccerBatch.set_persistent): W waves persistent, 0 one wave per "
+                         "block, -1 one wave per SIMD; default: the library's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ring-leg", action="store_true", help="skip the frame-ring leg timed beside the headline")
     ap.add_argument("--cpu-envs", type=int, default=65536)
@@ -191,6 +194,8 @@ def main():
         raise SystemExit("--frame-ring and --allgather are exclusive")
     batch = (FrameRingBatch(E, ring=ring, config=cfg, device=dev.index) if ring else
              SoccerBatch(E, config=cfg, device=dev.index))
+    if args.persistent is not None and not ring:
+        batch.set_persistent(args.persistent)
     batch.reset(seed=19 + rank * E)  # env i of rank r seeded 19 + r*E + i (global index)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
@@ -367,6 +372,9 @@ def main():
                                     else ""),
                        "envs_per_gpu": E, "global_envs": world * E, "max_steps": args.max_steps,
                        "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else ""),
+                       "launch": (f"persistent, {batch.persistent_waves} waves" if not ring and
+                                  batch.persistent_waves > 0 and (E + 63) // 64 > batch.persistent_waves
+                                  else "one wave per 64-env block"),
                        **({"obs_layout": f"frame ring, R = {ring} (opt-in; obs is a strided (N, 4, 66) window)"}
                           if ring else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

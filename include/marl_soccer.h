@@ -223,6 +223,14 @@ int ms_reset(ms_env *env, const uint64_t *pcg, const uint8_t *env_mask, int mode
 int ms_step(ms_env *env, const float *actions, float *obs, float *rew, uint8_t *term,
             uint8_t *trunc, int8_t *goal, int32_t *score);
 
+/* ms_step's launch shape. waves > 0: when the batch has more 64-env state blocks than that,
+ * ms_step runs a persistent grid of `waves` waves, wave w stepping blocks w, w + waves, ...
+ * with the first HBM batch of its next block loaded while it steps the current one (same
+ * results, bit for bit). waves = 0: one wave per block. waves < 0: one wave per SIMD of the
+ * device (4 x compute units), which is ms_create's default. Host-only. */
+int ms_set_persistent(ms_env *env, int waves);
+int ms_get_persistent(const ms_env *env);
+
 /* Frame-ring observations (opt-in; replaces the deque of 3 frames of soccer_env.py:130-140
  * and marl_vecenv.py:30-68 with a window into a longer per-agent ring, so a step writes one
  * frame instead of three). `frames`: device float [N][4][R][22], 16-B aligned, R even >= 4.

@@ -105,7 +105,7 @@ struct Counters {
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
     const unsigned long long act_ = __ballot(1);                                          \
     if ((int)(threadIdx.x & 63) == __ffsll((long long)act_) - 1 && S.stamps)              \
-      S.stamps[(int64_t)(blockIdx.x) * MS_NSTAMP + (k)] = t_;                                   \
+      S.stamps[stamp_row * MS_NSTAMP + (k)] = t_;                                               \
   } while (0)
 // cycles spent inside a region of a divergent loop, accumulated per lane; the wave's figure is
 // the maximum over its lanes (the lane that ran the most iterations), written to slot k
@@ -120,7 +120,7 @@ struct Counters {
       const unsigned long long x_ = __shfl_xor(m_, o_);                                  \
       m_ = x_ > m_ ? x_ : m_;                                                            \
     }                                                                                    \
-    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[(int64_t)blockIdx.x * MS_NSTAMP + (k)] = m_; \
+    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[stamp_row * MS_NSTAMP + (k)] = m_;       \
   } while (0)
 #else
 #define STAMP(k) do { } while (0)
@@ -949,6 +949,9 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
                                              Snap& h2, uint32_t pk0, bool need_h2) {
   const int lane = a.lane;
   const float dt = P.dt;
+#ifdef MS_STAMPS
+  const int64_t stamp_row = (a.blk - S.blocks) / BLOCK_BYTES;  // the state block (STAMP's row)
+#endif
   // cpBodyUpdatePosition
 #pragma unroll
   for (int b = 0; b < 5; ++b) {
@@ -1150,7 +1153,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
   {
     int mx = C.nc;
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[(int64_t)blockIdx.x * MS_NSTAMP + 12] = (unsigned long long)mx;
+    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[stamp_row * MS_NSTAMP + 12] = (unsigned long long)mx;
   }
 #endif
 
@@ -1255,19 +1258,6 @@ __device__ __forceinline__ void store_scalars(At a, const Env& E) {
                       (int32_t)E.meta, (int32_t)E.rng.u32);
 }
 
-// One env.step of every env (SoccerEnv.step -> Game.step, soccer_env.py:100-154,
-// game/game.py:378-437). Order inside a lane:
-//   1. the first HBM batch: scalars, bodies, actions, the old arbiter cache (entries < KC,
-//      staged in LDS) and PCG64; the t-1 snapshot (= the body state before this step) is
-//      staged in LDS;
-//   2. physics; the t-2 snapshot is loaded just before the solver and arrives while it runs;
-//      no other HBM read follows (gfx9 has one vmcnt for loads and stores, so a read after
-//      the stores would wait for them);
-//   3. goal, rewards, outputs, goal respawn, vec auto-reset;
-//   4. frames t-2, t-1, t of agent 0, then agent 1, ... (each 264-B row segment in one burst
-//      of stores, DESIGN.md §8), the history slot (t-1 becomes the next step's t-2) and the
-//      state. A lane whose stack is refilled (first step after a reset, or an auto-reset this
-//      step) writes three copies of frame t and the slot instead.
 // The reference's default config.json physics and rewards (make_params of ms_config_default,
 // bit for bit; ms_create compares the two and launches the specialised step kernel only when
 // they are identical). As compile-time constants the masses, restitution/friction products,
@@ -1291,63 +1281,112 @@ __host__ __device__ constexpr Params default_params() {
      {10.0f, 225.0f, 10.0f, 375.0f, -1.0f, 0.0f, 1.0f, {9.0f, 224.0f, 11.0f, 376.0f}},
      {790.0f, 225.0f, 790.0f, 375.0f, -1.0f, 0.0f, 1.0f, {789.0f, 224.0f, 791.0f, 376.0f}}}};
 }
-template <bool RING>
-__device__ __forceinline__ void step_envs(const DevState& S, const Params& P, const float* __restrict__ actions,
-                                          float* __restrict__ obs, float* __restrict__ rew,
-                                          uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                          int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
-                                          Counters* ctr, const Ring rg) {
-  __shared__ Lds L;
-  STAMP(0);
-  const int lane = threadIdx.x;
-  const int64_t e = (int64_t)blockIdx.x * MS_BLOCK + lane;
-  bool active = e < S.n;
-  // the wave's state block: a wave-uniform base (blockIdx.x) and this lane's slot in it
-  const At at{S.blocks + (int64_t)blockIdx.x * BLOCK_BYTES, lane};
-
-  // (1) loads, in the order their data is needed. They are unconditional (a padding lane of the
-  // last block reads its zeroed slot and the last env's actions): loads under a lane branch make
-  // the compiler copy the loaded registers at the join, and every copy waits for its load.
-  Env E;
-  load_scalars(at, E);
-  load_bodies(at, E);
-  Snap h2;  // obs-history snapshot t-2
-  float a[12];
-  {
-    const float4* ap = (const float4*)(actions + (active ? e : S.n - 1) * 12);
+// The first HBM batch of one state block (one wave's 64 envs): scalars, bodies, actions, the
+// previous step's arbiter-cache entries 0..KC-1 and PCG64. The scalars come first and alone
+// (fetch_scalars): the cache entries' addresses depend on them (parity bit, entry count).
+struct Fetch {
+  int4 sc;
+  float4 b[G_BODY];
+  float4 a[3];
+  uint32_t ch[KC];
+  float4 cj[KC];
+  ulonglong2 r0, r1;
+};
+__device__ __forceinline__ void fetch_scalars(const DevState& S, int64_t blk, int lane, Fetch& F) {
+  const At at{S.blocks + blk * BLOCK_BYTES, lane};
+  F.sc = *plane<int4>(at, OFF_I4, 0);
+}
+// Loads are unconditional (a padding lane of the last block reads its zeroed slot and the last
+// env's actions): loads under a lane branch make the compiler copy the loaded registers at the
+// join, and every copy waits for its load. A lane without cache entry k re-reads its own
+// scalars/bodies, which are in L1, instead.
+__device__ __forceinline__ void fetch_rest(const DevState& S, int64_t blk, int lane, const float* __restrict__ actions,
+                                           Fetch& F) {
+  const At at{S.blocks + blk * BLOCK_BYTES, lane};
+  const int64_t e = blk * MS_BLOCK + lane;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const float4 v = ap[q];
-      a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-    }
-  }
-  const int nco = META_NC(E.meta);
-  const int par0 = (E.meta & META_PAR) ? 1 : 0;
-  // old arbiter cache entries k < KC. No branch (so the compiler's wait counts stay exact): a
-  // lane without entry k re-reads its own scalars/bodies, which are in L1, instead.
-  uint32_t pch[KC];
-  float4 pcj[KC];
+  for (int g = 0; g < G_BODY; ++g) F.b[g] = *plane<float4>(at, OFF_B4, g);
+  const float4* ap = (const float4*)(actions + (e < S.n ? e : S.n - 1) * 12);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) F.a[q] = ap[q];
+  const uint32_t meta = (uint32_t)F.sc.z;
+  const int nco = META_NC(meta);
+  const int par0 = (meta & META_PAR) ? 1 : 0;
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
     const bool need = k < nco;
     const uint32_t* hp = need ? plane<uint32_t>(at, OFF_CH, par0 * MAXA + k) : (const uint32_t*)plane<int4>(at, OFF_I4, 0);
     const float4* jp = need ? plane<float4>(at, OFF_CJ, par0 * MAXA + k) : plane<float4>(at, OFF_B4, 0);
-    pch[k] = *hp;
-    pcj[k] = *jp;
+    F.ch[k] = *hp;
+    F.cj[k] = *jp;
   }
+  F.r0 = *plane<ulonglong2>(at, OFF_R2, 0);
+  F.r1 = *plane<ulonglong2>(at, OFF_R2, 1);
+}
+
+// One env.step of every env of state block `blk` (SoccerEnv.step -> Game.step,
+// soccer_env.py:100-154, game/game.py:378-437), one lane per env. Order inside a lane:
+//   1. the first HBM batch (Fetch, loaded by the caller): scalars, bodies, actions, the old
+//      arbiter cache (entries < KC, staged in LDS) and PCG64; the t-1 snapshot (= the body state
+//      before this step) is staged in LDS;
+//   2. physics; the t-2 snapshot is loaded just before the solver and arrives while it runs;
+//      no other HBM read follows (gfx9 has one vmcnt for loads and stores, so a read after
+//      the stores would wait for them), except PIPE's prefetch of the wave's next block, which
+//      is issued here, before any store of this block, so that it returns while this block's
+//      stores drain;
+//   3. goal, rewards, outputs, goal respawn, vec auto-reset;
+//   4. frames t-2, t-1, t of agent 0, then agent 1, ... (each 264-B row segment in one burst
+//      of stores, DESIGN.md §8), the history slot (t-1 becomes the next step's t-2) and the
+//      state. A lane whose stack is refilled (first step after a reset, or an auto-reset this
+//      step) writes three copies of frame t and the slot instead.
+template <bool RING, bool PIPE>
+__device__ __forceinline__ void step_block(const DevState& S, const Params& P, Lds& L, const int64_t blk, const Fetch& F,
+                                           const int64_t nblk_next, Fetch& N, const float* __restrict__ actions,
+                                           float* __restrict__ obs, float* __restrict__ rew,
+                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                           int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
+                                           Counters* ctr, const Ring rg) {
+  const int lane = threadIdx.x;
+  const int64_t e = blk * MS_BLOCK + lane;
+  bool active = e < S.n;
+  // the wave's state block: a wave-uniform base and this lane's slot in it
+  const At at{S.blocks + blk * BLOCK_BYTES, lane};
+#ifdef MS_STAMPS
+  const int64_t stamp_row = blk;
+#endif
+  STAMP(0);
+
+  Env E;
+  unpack_scalars(F.sc, E);
+  {
+    float f[44];
+#pragma unroll
+    for (int g = 0; g < G_BODY; ++g) {
+      f[4 * g] = F.b[g].x; f[4 * g + 1] = F.b[g].y; f[4 * g + 2] = F.b[g].z; f[4 * g + 3] = F.b[g].w;
+    }
+    unpack_bodies(f, E);
+  }
+  Snap h2;  // obs-history snapshot t-2
+  float a[12];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    a[4 * q] = F.a[q].x; a[4 * q + 1] = F.a[q].y; a[4 * q + 2] = F.a[q].z; a[4 * q + 3] = F.a[q].w;
+  }
+  const int nco = META_NC(E.meta);
   uint32_t pk0 = 0u;
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
-    L.u.np.ch[k][lane] = pch[k];
-    L.u.np.cj[k][lane] = pcj[k];
-    pk0 |= cache_key(pch[k]) << (8 * k);
+    L.u.np.ch[k][lane] = F.ch[k];
+    L.u.np.cj[k][lane] = F.cj[k];
+    pk0 |= cache_key(F.ch[k]) << (8 * k);
   }
-
-  stage_segments(P, L, lane);
+  if constexpr (PIPE) {  // the next block's scalars: their latency hides behind this block's physics
+    if (nblk_next >= 0) fetch_scalars(S, nblk_next, lane, N);
+  }
   bool fill3 = false, rng_dirty = false;
-  // PCG64 for goal respawns and auto-resets, with the first batch for every lane: 32 B/env
-  // more in the start burst instead of a dependent HBM round trip in most waves
-  load_rng(at, E);
+  E.rng.shi = F.r0.x; E.rng.slo = F.r0.y;
+  E.rng.ihi = F.r1.x; E.rng.ilo = F.r1.y;
+  E.rng.has32 = (E.meta & META_H32) ? 1u : 0u;
   Snap h1;  // obs-history snapshot t-1: the body state before this step
   if (active) {
     // SoccerEnv.step validation (soccer_env.py:101-117): a non-finite action skips the env
@@ -1381,18 +1420,18 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     for (int b = 0; b < 5; ++b) { pvx[b] = E.px[b]; pvy[b] = E.py[b]; }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float F[3];
+      float Fo[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         float v = a[i * 3 + k];
         v = v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v);
-        F[k] = v * (k < 2 ? P.force_max : P.torque_max);
+        Fo[k] = v * (k < 2 ? P.force_max : P.torque_max);
       }
-      float s, c;
-      sincos_contract(E.ang[i], &s, &c);
-      fx[i] = 0.0f + (c * F[0] + (-s) * F[1]);
-      fy[i] = 0.0f + (s * F[0] + c * F[1]);
-      tq[i] = F[2];
+      float sn, cs;
+      sincos_contract(E.ang[i], &sn, &cs);
+      fx[i] = 0.0f + (cs * Fo[0] + (-sn) * Fo[1]);
+      fy[i] = 0.0f + (sn * Fo[0] + cs * Fo[1]);
+      tq[i] = Fo[2];
     }
 
     unsigned long long ovf = 0;
@@ -1410,7 +1449,11 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
     for (int b = 0; b < 5; ++b) { pvx[b] = h1.px[b]; pvy[b] = h1.py[b]; }
     STAMP(7);
     if (ovf) atomicAdd(&ctr->overflow, ovf);
-
+  }
+  if constexpr (PIPE) {  // the rest of the next block's first batch, ahead of this block's stores
+    if (nblk_next >= 0) fetch_rest(S, nblk_next, lane, actions, N);
+  }
+  if (active) {
     // goal detection (game.py:401-412)
     int goal = 0;
     const float bx = E.px[4], by = E.py[4];
@@ -1473,10 +1516,44 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if (lane == 0) {
-      uint4* t = S.tally + blockIdx.x;
+      uint4* t = S.tally + blk;
       atomicAdd(&t->x, v & 0xfffu);
       atomicAdd(&t->y, (v >> 12) & 0xfffu);
       atomicAdd(&t->z, v >> 24);
+    }
+  }
+}
+
+// One wave per state block (grid = blocks), or PIPE: a persistent grid of waves, wave w taking
+// blocks w, w + grid, w + 2 grid, ... with the first batch of its next block loaded during the
+// current one (issued before the current block's stores, so it returns while they drain and the
+// next block starts without the start-of-kernel load burst: DESIGN.md §6).
+template <bool RING, bool PIPE>
+__device__ __forceinline__ void step_envs(const DevState& S, const Params& P, const float* __restrict__ actions,
+                                          float* __restrict__ obs, float* __restrict__ rew,
+                                          uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                          int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
+                                          Counters* ctr, const Ring rg) {
+  __shared__ Lds L;
+  const int lane = threadIdx.x;
+  int64_t blk = blockIdx.x;
+  Fetch F;
+  fetch_scalars(S, blk, lane, F);
+  fetch_rest(S, blk, lane, actions, F);
+  stage_segments(P, L, lane);
+  if constexpr (!PIPE) {
+    step_block<RING, false>(S, P, L, blk, F, -1, F, actions, obs, rew, term, trunc, goal_out, score_out, ctr, rg);
+  } else {
+    const int64_t nblk = (S.n + MS_BLOCK - 1) / MS_BLOCK;
+#pragma unroll 1
+    for (;;) {
+      const int64_t nb = blk + gridDim.x;
+      Fetch N;
+      step_block<RING, true>(S, P, L, blk, F, nb < nblk ? nb : -1, N, actions, obs, rew, term, trunc, goal_out,
+                             score_out, ctr, rg);
+      if (nb >= nblk) break;
+      blk = nb;
+      F = N;
     }
   }
 }
@@ -1492,9 +1569,28 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params Pi
     Params Pd = default_params();
     Pd.max_steps = Pin.max_steps;  // episode length and auto-reset stay runtime values
     Pd.autoreset = Pin.autoreset;
-    step_envs<false>(S, Pd, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
+    step_envs<false, false>(S, Pd, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
   } else {
-    step_envs<false>(S, Pin, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
+    step_envs<false, false>(S, Pin, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
+  }
+}
+
+// ms_step over more blocks than the GPU holds waves at once: a persistent grid, each wave
+// stepping several blocks with its next block's first batch prefetched (step_envs PIPE)
+template <bool DEFAULT_PARAMS>
+__global__ __launch_bounds__(MS_BLOCK) void ms_step_pipe_kernel(DevState S, Params Pin, const float* __restrict__ actions,
+                                                                float* __restrict__ obs, float* __restrict__ rew,
+                                                                uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                                int8_t* __restrict__ goal_out,
+                                                                int32_t* __restrict__ score_out, Counters* ctr) {
+  const Ring none{nullptr, 0, 0, 0};
+  if constexpr (DEFAULT_PARAMS) {
+    Params Pd = default_params();
+    Pd.max_steps = Pin.max_steps;
+    Pd.autoreset = Pin.autoreset;
+    step_envs<false, true>(S, Pd, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
+  } else {
+    step_envs<false, true>(S, Pin, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
   }
 }
 
@@ -1509,9 +1605,9 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_ring_kernel(DevState S, Para
     Params Pd = default_params();
     Pd.max_steps = Pin.max_steps;
     Pd.autoreset = Pin.autoreset;
-    step_envs<true>(S, Pd, actions, nullptr, rew, term, trunc, goal_out, score_out, ctr, rg);
+    step_envs<true, false>(S, Pd, actions, nullptr, rew, term, trunc, goal_out, score_out, ctr, rg);
   } else {
-    step_envs<true>(S, Pin, actions, nullptr, rew, term, trunc, goal_out, score_out, ctr, rg);
+    step_envs<true, false>(S, Pin, actions, nullptr, rew, term, trunc, goal_out, score_out, ctr, rg);
   }
 }
 
@@ -1668,6 +1764,7 @@ struct ms_env {
   int device;
   hipStream_t stream;
   int64_t n;
+  int pipe_waves;  // ms_step: > 0 persistent grid of this many waves (0: one wave per block)
   Params P;
   bool default_params;  // P == default_params() up to max_steps/autoreset: specialised kernel
   DevState S;
@@ -1857,6 +1954,11 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
   if (cfg) h->cfg = *cfg; else ms_config_default(&h->cfg);
   make_params(&h->cfg, &h->P);
   h->default_params = params_are_default(h->P);
+  {  // ms_step's default launch shape: persistent once the batch outgrows one wave per SIMD
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    h->pipe_waves = 4 * cus;
+  }
   const size_t n = (size_t)n_envs;
   const size_t total = (size_t)((n + BLK - 1) / BLK) * BLOCK_BYTES;  // state blocks, the last one padded
   char* base = nullptr;
@@ -1953,15 +2055,38 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
   if (((uintptr_t)actions & 15u) || ((uintptr_t)obs & 7u) || ((uintptr_t)rew & 15u) || ((uintptr_t)term & 3u) ||
       ((uintptr_t)trunc & 3u) || ((uintptr_t)score & 7u))
     return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: misaligned buffer (actions/rew 16 B, obs/score 8 B, flags 4 B)");
-  if (h->default_params)
-    hipLaunchKernelGGL(ms_step_kernel<true>, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S, h->P,
-                       actions, obs, rew, term, trunc, goal, score, h->ctr);
-  else
-    hipLaunchKernelGGL(ms_step_kernel<false>, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S,
-                       h->P, actions, obs, rew, term, trunc, goal, score, h->ctr);
+  const unsigned nblk = grid_for(h->n, MS_BLOCK);
+  if (h->pipe_waves > 0 && nblk > (unsigned)h->pipe_waves) {
+    const dim3 grid((unsigned)h->pipe_waves);
+    if (h->default_params)
+      hipLaunchKernelGGL(ms_step_pipe_kernel<true>, grid, dim3(MS_BLOCK), 0, h->stream, h->S, h->P, actions, obs, rew,
+                         term, trunc, goal, score, h->ctr);
+    else
+      hipLaunchKernelGGL(ms_step_pipe_kernel<false>, grid, dim3(MS_BLOCK), 0, h->stream, h->S, h->P, actions, obs,
+                         rew, term, trunc, goal, score, h->ctr);
+  } else if (h->default_params) {
+    hipLaunchKernelGGL(ms_step_kernel<true>, dim3(nblk), dim3(MS_BLOCK), 0, h->stream, h->S, h->P, actions, obs, rew,
+                       term, trunc, goal, score, h->ctr);
+  } else {
+    hipLaunchKernelGGL(ms_step_kernel<false>, dim3(nblk), dim3(MS_BLOCK), 0, h->stream, h->S, h->P, actions, obs,
+                       rew, term, trunc, goal, score, h->ctr);
+  }
   HIPCHK(hipGetLastError());
   return MS_OK;
 }
+
+int ms_set_persistent(ms_env* h, int waves) {
+  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_persistent: null handle");
+  if (waves < 0) {  // automatic: one wave per SIMD (four per CU: 39 KB of LDS per wave)
+    int cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+    waves = 4 * cus;
+  }
+  h->pipe_waves = waves;
+  return MS_OK;
+}
+
+int ms_get_persistent(const ms_env* h) { return h ? h->pipe_waves : -1; }
 
 // Frame-ring arguments: frames 16-B aligned, R even and >= 4, window pos..pos+2 inside the row.
 static int ring_check(const char* fn, const float* frames, int R, int pos, int wrap) {
