@@ -132,6 +132,31 @@ struct Counters {
 #endif
 #define MS_NSTAMP 24
 
+// Diagnostic builds only (tools/maxilp_bisect.sh): a scheduling barrier at a phase boundary
+// when MS_SB_<phase> is defined, to find which region's instruction schedule changes results
+// under LLVM's max-ILP AMDGPU scheduler ("Faults"). Empty in the product build.
+#define MS_SB_IF(on) do { if (on) __builtin_amdgcn_sched_barrier(0); } while (0)
+#ifdef MS_SB_SOLVER
+#define MS_SB_SOLVER_ON 1
+#else
+#define MS_SB_SOLVER_ON 0
+#endif
+#ifdef MS_SB_NARROW
+#define MS_SB_NARROW_ON 1
+#else
+#define MS_SB_NARROW_ON 0
+#endif
+#ifdef MS_SB_PRESTEP
+#define MS_SB_PRESTEP_ON 1
+#else
+#define MS_SB_PRESTEP_ON 0
+#endif
+#ifdef MS_SB_OBS
+#define MS_SB_OBS_ON 1
+#else
+#define MS_SB_OBS_ON 0
+#endif
+
 // ---- per-lane env register file ------------------------------------------------------------
 struct Env {
   float px[5], py[5], vx[5], vy[5], ang[4], w[5], vbx[5], vby[5], wb[5];
@@ -1024,6 +1049,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
 #endif
   // narrowphase, one compacted loop per pair class so each lane visits only its own touching
   // pairs; class order + ctz order = canonical pair order (DESIGN.md pair table)
+  MS_SB_IF(MS_SB_NARROW_ON);
   while (mAA) {
     const int p = __builtin_ctz(mAA);
     mAA &= mAA - 1;
@@ -1142,6 +1168,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     if (col.count) add_arbiter(a, L, C, ovf, W, 42 + s, 4, 5, col, v2(0.0f, 0.0f), v2(0.0f, 0.0f), overflow_acc);
   }
   while (W.cur < W.nc_old) cache_age_current(a, L, W, overflow_acc);
+  MS_SB_IF(MS_SB_NARROW_ON);
   // contacts KREG.. of a pile-up from the global spill into LDS for the 12 passes over them
   // (the narrowphase scratch they share LDS with is dead from here on)
   asm volatile("" ::: "memory");
@@ -1167,6 +1194,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     if (__ballot(PRE_GROUP * g < C.nc) != 0) {
       static_for<0, PRE_GROUP>([&](auto kc) __attribute__((always_inline)) {
         prestep_one(P, C.reg[PRE_GROUP * g + decltype(kc)::value], L, lane);
+        MS_SB_IF(MS_SB_PRESTEP_ON);
       });
     }
   });
@@ -1207,12 +1235,13 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
   if (need_h2) snap_load(a, h2);  // arrives during the solver
   if (C.nc > 0) {
     // cpArbiterApplyCachedImpulse, then cpArbiterApplyImpulse x 10 (pymunk Space default)
-    FOR_CONTACTS(C, ovf, warm_one(P, c_, L, lane));
+    MS_SB_IF(MS_SB_SOLVER_ON);
+    FOR_CONTACTS(C, ovf, { warm_one(P, c_, L, lane); MS_SB_IF(MS_SB_SOLVER_ON); });
     STAMP(15);
 #pragma unroll 1
     for (int it = 0; it < 10; ++it) {
       asm volatile("; MS_SOLVER_ITER_BEGIN" ::: "memory");
-      FOR_CONTACTS(C, ovf, solve_one(P, c_, L, lane));
+      FOR_CONTACTS(C, ovf, { solve_one(P, c_, L, lane); MS_SB_IF(MS_SB_SOLVER_ON); });
       asm volatile("; MS_SOLVER_ITER_END" ::: "memory");
     }
     STAMP(5);
@@ -1497,6 +1526,7 @@ __device__ __forceinline__ void step_block(const DevState& S, const Params& P, L
       emit_fill3(at, P, e, s0, obs);
       E.meta &= ~META_HE;
     } else {
+      MS_SB_IF(MS_SB_OBS_ON);
       if (obs) emit_three(P, h2, h1, s0, obs + e * 264);
       snap_store(at, h1);  // t-1 becomes the next step's t-2
     }
