@@ -262,6 +262,26 @@ int ms_debug_rewards(ms_env *env, const float *prev_pos, const float *cur_pos,
                      const int8_t *goal, const uint8_t *terminal, const int32_t *score,
                      float *rew);
 
+/* ---- policy forward (the env's immediate caller: SURVEY.md §8(f) rank 1) -------------------
+ * ms_policy_forward <- the reference rollout's per-step policy evaluation (marl-soccer.ipynb
+ * train cell L299-313; eval.py:69-81): RunningMeanStd normalisation of the blue agents' obs
+ * (clip((x - mean) / (sqrt(var) + 1e-8), -10, 10) in float64, then float32) followed by the
+ * notebook Agent's two tanh MLPs 66-512-256-128-64-{3, 1} (actor mean, critic value;
+ * eval.py:17-47), fused in one gfx950 kernel (f32-input MFMA, activations in registers).
+ *   x: device float rows of 66; row r at x + (r / group_rows) * group_stride +
+ *      (r % group_rows) * row_stride floats (the blue agents of an (N, 4, 66) obs buffer:
+ *      rows 2N, group_rows 2, group_stride 264, row_stride 66).
+ *   mean, den: device float64 [66]: the normaliser's mean and sqrt(var) + 1e-8, or both NULL
+ *      for rows that are normalised already.
+ *   actor, critic: device packed nets (MS_POLICY_NET_FLOATS floats each, 16-B aligned; the
+ *      layout is marlsoccer/policy.py pack_net's; either may be NULL to skip that net).
+ *   act_mean: device float [rows][3]; value: device float [rows]. Asynchronous on `stream`. */
+#define MS_POLICY_NET_FLOATS 211936
+int ms_policy_forward(const float *x, int64_t rows, int group_rows, int64_t group_stride, int64_t row_stride,
+                      const double *mean, const double *den, const float *actor, const float *critic,
+                      float *act_mean, float *value, void *stream);
+const char *ms_policy_last_error(void);
+
 /* Synchronises the stream and reads the device counters. */
 int ms_get_stats(ms_env *env, ms_stats *out);
 int ms_reset_stats(ms_env *env);

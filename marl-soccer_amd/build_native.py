@@ -18,7 +18,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libmarlsoccer.so")
-SOURCES = [os.path.join(CSRC, "ms_env.hip")]
+SOURCES = [os.path.join(CSRC, "ms_env.hip"), os.path.join(CSRC, "ms_policy.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, "ms_device.h"), os.path.join(ROOT, "include", "marl_soccer.h")]
 ARCH = os.environ.get("MS_OFFLOAD_ARCH", "gfx950")
 # LLVM's default AMDGPU machine scheduler. The max-ILP strategy (-mllvm

@@ -284,3 +284,66 @@ def test_evaluate_argument_errors_before_any_device_work():
         evaluate(agent, rms, 4, red="greedy")
     with pytest.raises(ValueError, match="graph=True cannot take frames"):
         evaluate(agent, rms, 4, graph=True, frames_every=10)
+
+
+@pytest.mark.gpu
+def test_fused_policy_kernel_matches_reference_network():
+    """ms_policy_forward (csrc/ms_policy.hip: both MLPs in one gfx950 kernel on the f32-input
+    MFMA) on the notebook Agent's golden vectors: the actor mean and the value within 1e-5 of
+    the reference network's outputs (policy.npz, produced by the notebook's own class); and on
+    131 random rows (a ragged last tile) within 1e-5 of the same Agent run by torch on the GPU."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer.policy import FusedPolicy
+    torch.manual_seed(0)
+    agent = Agent().cuda()
+    fp = FusedPolicy(agent)
+    x = torch.from_numpy(FX["x"]).cuda()
+    mean, value = fp.forward(x)
+    np.testing.assert_allclose(mean.cpu().numpy(), FX["mean"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(value.cpu().numpy(), FX["value"][:, 0], rtol=0, atol=1e-5)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    x = (torch.randn((131, 66), generator=g, device="cuda") * 3).clamp(-10, 10)
+    with torch.no_grad():
+        rm, rv = agent.actor_mean(x), agent.critic(x)[:, 0]
+    mean, value = fp.forward(x)
+    np.testing.assert_allclose(mean.cpu().numpy(), rm.cpu().numpy(), rtol=0, atol=1e-5)
+    np.testing.assert_allclose(value.cpu().numpy(), rv.cpu().numpy(), rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_fused_policy_kernel_normalises_like_running_mean_std():
+    """The kernel's fused normalisation of raw (N, 4, 66) env observations (blue agents: rows
+    2N, row 2e + a at obs[e, a]) equals RunningMeanStd.normalize followed by the torch Agent,
+    within 1e-5, with the run5 normaliser stats of the reference (policy.npz) and after a
+    parameter update (pack() re-reads the parameters)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer import SoccerBatch
+    from marlsoccer.policy import FusedPolicy
+    n = 1000
+    env = SoccerBatch(n)
+    env.reset(seed=7)
+    for t in range(5):
+        env.step(torch.rand((n, 4, 3), device=env.device) * 2 - 1)
+    torch.manual_seed(1)
+    agent = Agent().to(env.device)
+    rms = RunningMeanStd(device=env.device)
+    rms.mean.copy_(torch.from_numpy(FX["run5_mean"]))
+    rms.var.copy_(torch.from_numpy(FX["run5_var"]))
+    fp = FusedPolicy(agent)
+    for it in range(2):
+        obs = env.obs
+        den = rms.std + 1e-8
+        mean, value = fp.forward(obs, rms.mean, den, group_rows=2, group_stride=264, row_stride=66, rows=2 * n)
+        with torch.no_grad():
+            xn = rms.normalize(obs[:, :2].reshape(-1, 66))
+            rm, rv = agent.actor_mean(xn), agent.critic(xn)[:, 0]
+        np.testing.assert_allclose(mean.cpu().numpy(), rm.cpu().numpy(), rtol=0, atol=1e-5)
+        np.testing.assert_allclose(value.cpu().numpy(), rv.cpu().numpy(), rtol=0, atol=1e-5)
+        with torch.no_grad():  # a parameter update, then re-pack
+            for p in agent.parameters():
+                p.add_(0.01 * torch.randn_like(p))
+        fp.pack()
+    env.close()

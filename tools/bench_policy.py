@@ -4,9 +4,11 @@
 
     python tools/bench_policy.py [--envs 65536] [--iters 20]
 
-a) nn.Sequential fp32 (DeviceRollout today), b) both MLPs as one 66->1024 GEMM + batched
-(2, M, k) GEMMs per layer (fp32), c) a) under bf16 autocast, d) b) in bf16. Prints ms per
-forward and the max |difference| of the action mean and value against a).
+a) nn.Sequential fp32 (hipBLASLt GEMMs + tanh passes), b) both MLPs as one 66->1024 GEMM +
+batched (2, M, k) GEMMs per layer (fp32), c) a) under bf16 autocast, d) b) in bf16, e) the
+fused gfx950 kernel ms_policy_forward (f32-input MFMA, activations in registers; marlsoccer.policy),
+f) e) with the RunningMeanStd normalisation fused (raw rows in, float64 normalisation in-kernel).
+Prints ms per forward and the max |difference| of the action mean and value against a).
 """
 from __future__ import annotations
 
@@ -59,11 +61,28 @@ def main():
         return mu.float(), v.float()
 
     p32, p16 = pack(torch.float32), pack(torch.bfloat16)
+    from marlsoccer.policy import FusedPolicy
+    fp = FusedPolicy(agent)
+    am = torch.empty((M, 3), device=dev)
+    vv = torch.empty((M,), device=dev)
+    mean0 = torch.zeros(66, dtype=torch.float64, device=dev)
+    den1 = torch.full((66,), 1.0 + 1e-8, dtype=torch.float64, device=dev)
+
+    def kern():
+        fp.forward(x, act_mean=am, value=vv)
+        return am, vv[:, None]
+
+    def kern_norm():
+        fp.forward(x, mean0, den1, act_mean=am, value=vv)
+        return am, vv[:, None]
+
     variants = {
         "sequential_fp32": seq,
         "fused_fp32": lambda: fused(p32, torch.float32),
         "sequential_bf16_autocast": lambda: torch.autocast("cuda", dtype=torch.bfloat16)(seq)(),
         "fused_bf16": lambda: fused(p16, torch.bfloat16),
+        "ms_policy_forward": kern,
+        "ms_policy_forward_normalising": kern_norm,
     }
     with torch.no_grad():
         ref_mu, ref_v = seq()
@@ -78,7 +97,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
-            print(json.dumps({"variant": name, "rows": M, "ms_per_forward": ms,
+            print(json.dumps({"variant": name, "rows": M, "ms_per_forward": ms, "tflops": 824192 * 2 * M / 2 / ms / 1e9,
                               "max_abs_diff_mean": float((mu.float() - ref_mu).abs().max()),
                               "max_abs_diff_value": float((v.float() - ref_v).abs().max())}), flush=True)
 

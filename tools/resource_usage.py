@@ -20,9 +20,11 @@ def main(tag, extra=()):
     import build_native
 
     flags = [f for f in build_native.FLAGS if f not in ("-shared",)]
-    cmd = [build_native.hipcc(), *flags, *extra, "-Rpass-analysis=kernel-resource-usage", "--cuda-device-only",
-           "-c", "-o", os.devnull, *build_native.SOURCES]
-    out = subprocess.run(cmd, capture_output=True, text=True, check=True).stderr
+    out = ""
+    for src in build_native.SOURCES:
+        cmd = [build_native.hipcc(), *flags, *extra, "-Rpass-analysis=kernel-resource-usage", "--cuda-device-only",
+               "-c", "-o", os.devnull, src]
+        out += subprocess.run(cmd, capture_output=True, text=True, check=True).stderr
     lines = []
     for ln in out.splitlines():
         m = re.search(r"remark:\s+(.*?)\s+\[-Rpass-analysis", ln)
