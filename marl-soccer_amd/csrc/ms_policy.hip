@@ -36,6 +36,14 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int TM = 32;  // rows per wave
+#ifndef MS_POL_DEPTH
+#define MS_POL_DEPTH 2
+#endif
+#ifndef MS_POL_CH
+#define MS_POL_CH 4
+#endif
+constexpr int DEPTH = MS_POL_DEPTH;  // A-operand groups in flight
+constexpr int CH = MS_POL_CH;        // output tiles accumulated at once (layers 1-3)
 constexpr int T1 = 16, T2 = 8, T3 = 4, T4 = 2, T5 = 1;
 constexpr int G1 = 9, G2 = 64, G3 = 32, G4 = 16, G5 = 8;
 constexpr int OW1 = 0, OB1 = OW1 + T1 * G1 * 256;
@@ -77,17 +85,24 @@ __device__ __forceinline__ void dense(BOP&& bop, f32x16 (&Y)[T_OUT], const float
       acc[decltype(tc)::value] = f32x16{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
                                         0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     });
-    f32x4 a[2][CH];  // this group's and the next group's A operands
-    static_for<0, CH>([&](auto tc) __attribute__((always_inline)) {
-      constexpr int t = decltype(tc)::value;
-      a[0][t] = *(const f32x4*)(W + (((c * CH + t) * G + 0) * 64 + lane) * 4);
+    // A operands of the current group and the next DEPTH - 1 groups (a ring: each group's
+    // 16-B loads are issued DEPTH - 1 groups, 4 (DEPTH - 1) CH MFMAs, ahead of their use)
+    f32x4 a[DEPTH][CH];
+    static_for<0, DEPTH - 1>([&](auto pc) __attribute__((always_inline)) {
+      constexpr int g = decltype(pc)::value;
+      if constexpr (g < G) {
+        static_for<0, CH>([&](auto tc) __attribute__((always_inline)) {
+          constexpr int t = decltype(tc)::value;
+          a[g][t] = *(const f32x4*)(W + (((c * CH + t) * G + g) * 64 + lane) * 4);
+        });
+      }
     });
     static_for<0, G>([&](auto gc) __attribute__((always_inline)) {
       constexpr int g = decltype(gc)::value;
-      if constexpr (g + 1 < G) {
+      if constexpr (g + DEPTH - 1 < G) {
         static_for<0, CH>([&](auto tc) __attribute__((always_inline)) {
           constexpr int t = decltype(tc)::value;
-          a[(g + 1) & 1][t] = *(const f32x4*)(W + (((c * CH + t) * G + g + 1) * 64 + lane) * 4);
+          a[(g + DEPTH - 1) % DEPTH][t] = *(const f32x4*)(W + (((c * CH + t) * G + g + DEPTH - 1) * 64 + lane) * 4);
         });
       }
       static_for<0, 4>([&](auto jc) __attribute__((always_inline)) {
@@ -95,7 +110,7 @@ __device__ __forceinline__ void dense(BOP&& bop, f32x16 (&Y)[T_OUT], const float
         const float bv = bop(std::integral_constant<int, 4 * g + j>{});
         static_for<0, CH>([&](auto tc) __attribute__((always_inline)) {
           constexpr int t = decltype(tc)::value;
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g & 1][t][j], bv, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g % DEPTH][t][j], bv, acc[t], 0, 0, 0);
         });
       });
     });
@@ -121,15 +136,15 @@ __device__ __forceinline__ void dense(BOP&& bop, f32x16 (&Y)[T_OUT], const float
 // s < 36; steps 33-35 are zero). Returns the last layer's tile (rows 0..NOUT-1 of lane half 0).
 __device__ __forceinline__ f32x16 net_forward(const float (&xk)[36], const float* __restrict__ P, int lane) {
   f32x16 H1[T1];
-  dense<T1, G1, 4, false>([&](auto s) __attribute__((always_inline)) { return xk[decltype(s)::value]; }, H1, P + OW1,
+  dense<T1, G1, CH, false>([&](auto s) __attribute__((always_inline)) { return xk[decltype(s)::value]; }, H1, P + OW1,
                           P + OB1, lane);
   f32x16 H2[T2];
-  dense<T2, G2, 4, false>([&](auto s) __attribute__((always_inline)) {
+  dense<T2, G2, CH, false>([&](auto s) __attribute__((always_inline)) {
     constexpr int k = decltype(s)::value;
     return H1[k >> 4][k & 15];
   }, H2, P + OW2, P + OB2, lane);
   f32x16 H3[T3];
-  dense<T3, G3, 4, false>([&](auto s) __attribute__((always_inline)) {
+  dense<T3, G3, CH, false>([&](auto s) __attribute__((always_inline)) {
     constexpr int k = decltype(s)::value;
     return H2[k >> 4][k & 15];
   }, H3, P + OW3, P + OB3, lane);

@@ -69,6 +69,8 @@ def evaluate(agent: Agent, normalizer: RunningMeanStd, num_episodes: int, seed=N
             eager = max_steps - chunk * ((max_steps - 1) // chunk) if max_steps > 1 else 1
             for _ in range(eager):
                 body()
+            replays = (max_steps - eager) // chunk
+        if graph and replays > 0:
             g = torch.cuda.CUDAGraph()
             g.register_generator_state(gen)
             cur = torch.cuda.current_stream(dev)
@@ -83,9 +85,9 @@ def evaluate(agent: Agent, normalizer: RunningMeanStd, num_episodes: int, seed=N
             finally:
                 batch.set_stream(old)
             cur.wait_stream(s)
-            for _ in range((max_steps - eager) // chunk):
+            for _ in range(replays):
                 g.replay()
-        else:
+        elif not graph:
             for t in range(max_steps):
                 body()
                 if frames_every and (t % frames_every == 0 or t == max_steps - 1):

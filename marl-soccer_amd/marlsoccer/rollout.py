@@ -150,12 +150,16 @@ class DeviceRollout:
     second captures its num_steps steps as one HIP graph and replays it, and later calls replay
     that graph — one launch per rollout instead of ~40 kernel launches per step. The captured
     graph reads the agent's parameters and the normalizer's mean/var in place, so the PPO
-    update must modify them in place (optimizer steps and RunningMeanStd.update do).
+    update must modify them in place (optimizer steps and RunningMeanStd.update do); a replay
+    checks that those tensors are still the captured ones and captures again if not.
+    policy="fused" (the default for fp32): the normalisation and both MLPs run as ONE gfx950
+    kernel (ms_policy_forward: f32-input MFMA, activations in registers; marlsoccer.policy),
+    within 1e-5 of the torch modules; "torch": the modules themselves (hipBLASLt GEMMs).
     """
 
     def __init__(self, batch, agent: Agent, normalizer: RunningMeanStd, num_steps: int, seed: int = 0,
                  deterministic: bool = False, update_normalizer: bool = True, graph: bool = False,
-                 policy_dtype: torch.dtype = torch.float32):
+                 policy_dtype: torch.dtype = torch.float32, policy: str | None = None):
         self.batch, self.agent, self.normalizer = batch, agent, normalizer
         self.T, self.N = int(num_steps), batch.num_envs
         self.deterministic = deterministic
@@ -164,7 +168,20 @@ class DeviceRollout:
         if policy_dtype not in (torch.float32, torch.bfloat16):
             raise ValueError(f"policy_dtype must be torch.float32 or torch.bfloat16, got {policy_dtype}")
         self.policy_dtype = policy_dtype
+        if policy is None:
+            policy = "fused" if policy_dtype == torch.float32 else "torch"
+        if policy not in ("fused", "torch") or (policy == "fused" and policy_dtype != torch.float32):
+            raise ValueError(f"policy must be 'fused' (fp32) or 'torch', got {policy!r} with {policy_dtype}")
+        self.policy = policy
+        self._fused = None
+        if policy == "fused":
+            from .policy import FusedPolicy
+            self._fused = FusedPolicy(agent)
+            self._am = torch.zeros((batch.num_envs * 2, ACT_DIM), dtype=torch.float32, device=batch.device)
+            self._val = torch.zeros((batch.num_envs * 2,), dtype=torch.float32, device=batch.device)
+            self._den = torch.ones((OBS_DIM,), dtype=torch.float64, device=batch.device)
         self._graph = None
+        self._graph_inputs = None
         self._collects = 0
         dev = batch.device
         self.gen = torch.Generator(device=dev)
@@ -187,18 +204,26 @@ class DeviceRollout:
         b = self.batch
         self.obs[t] = self.next_obs
         self.dones[t] = self.next_done
-        x = self.normalizer.normalize(self.next_obs.reshape(-1, OBS_DIM))
-        # no autocast weight-cast cache: its casts would be allocated and reused across a graph
-        # capture (the casts of ~0.4 M parameters per step are negligible)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.policy_dtype == torch.bfloat16,
-                            cache_enabled=False):
+        if self._fused is not None:
+            # normalisation + actor + critic in one kernel, straight from the (N, 2, 66) obs rows
+            self._fused.forward(self.next_obs, self.normalizer.mean, self._den, act_mean=self._am, value=self._val)
+            action_mean, value = self._am, self._val
             if self.deterministic:
-                action = self.agent.get_deterministic_action(x)
-                value = self.agent.get_value(x)
-                logprob = torch.zeros(x.shape[0], device=x.device)
-            else:
-                action_mean = self.agent.actor_mean(x).float()
-                value = self.agent.get_value(x)
+                action = action_mean
+                logprob = torch.zeros(action_mean.shape[0], device=action_mean.device)
+        else:
+            x = self.normalizer.normalize(self.next_obs.reshape(-1, OBS_DIM))
+            # no autocast weight-cast cache: its casts would be allocated and reused across a graph
+            # capture (the casts of ~0.4 M parameters per step are negligible)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.policy_dtype == torch.bfloat16,
+                                cache_enabled=False):
+                if self.deterministic:
+                    action = self.agent.get_deterministic_action(x)
+                    value = self.agent.get_value(x)
+                    logprob = torch.zeros(x.shape[0], device=x.device)
+                else:
+                    action_mean = self.agent.actor_mean(x).float()
+                    value = self.agent.get_value(x)
         if not self.deterministic:
             action, logprob = self.agent.sample(action_mean, generator=self.gen)
         self.values[t] = value.reshape(self.N, 2)
@@ -216,9 +241,18 @@ class DeviceRollout:
         self.episodes += finished.sum()
         self.score_sum += (b.score * finished[:, None]).sum(dim=0)
 
+    @torch.no_grad()
     def _run_steps(self) -> None:
+        if self._fused is not None:  # the parameters and the normaliser as they are now
+            self._fused.pack()
+            torch.add(self.normalizer.std, 1e-8, out=self._den)
         for t in range(self.T):
             self.step(t)
+
+    def _inputs_identity(self) -> tuple:
+        """The tensors a captured rollout reads in place (their storage)."""
+        return tuple(p.data_ptr() for p in self.agent.parameters()) + (self.normalizer.mean.data_ptr(),
+                                                                          self.normalizer.var.data_ptr())
 
     def _capture(self) -> None:
         b, dev = self.batch, self.batch.device
@@ -238,8 +272,11 @@ class DeviceRollout:
 
     def collect(self) -> dict:
         if self.graph and self._collects > 0:
+            if self._graph is not None and self._graph_inputs != self._inputs_identity():
+                self._graph = None  # parameters or normaliser tensors were replaced: capture again
             if self._graph is None:
                 self._capture()  # records only; the replay below runs it
+                self._graph_inputs = self._inputs_identity()
             self._graph.replay()
         else:
             self._run_steps()

@@ -141,8 +141,9 @@ def test_graph_rollout_matches_eager_rollout():
 
 @pytest.mark.gpu
 def test_device_rollout_deterministic_matches_host_loop():
-    """Deterministic rollout == the eval.py-style host loop (policy mean for blue, the same
-    red actions) step for step."""
+    """Deterministic rollout (torch policy) == the eval.py-style host loop (policy mean for blue,
+    the same red actions) step for step; the fused-kernel rollout's first actions are within
+    1e-5 of the same loop's."""
     if not torch.cuda.is_available():
         pytest.skip("needs a HIP device")
     from marlsoccer import SoccerBatch
@@ -153,7 +154,9 @@ def test_device_rollout_deterministic_matches_host_loop():
     b1, b2 = SoccerBatch(N), SoccerBatch(N)
     b1.reset(seed=7)
     b2.reset(seed=7)
-    ro = DeviceRollout(b1, agent, rms, T, seed=9, deterministic=True, update_normalizer=False)
+    # the torch policy, so that the host loop below can use the same modules bit for bit (the
+    # fused kernel's outputs are within 1e-5 of them: test_fused_policy_*)
+    ro = DeviceRollout(b1, agent, rms, T, seed=9, deterministic=True, update_normalizer=False, policy="torch")
     out = ro.collect()
     g = torch.Generator(device="cuda")
     g.manual_seed(9)
@@ -168,6 +171,16 @@ def test_device_rollout_deterministic_matches_host_loop():
     assert torch.equal(b1.obs, b2.obs) and torch.equal(b1.rew, b2.rew)
     b1.close()
     b2.close()
+    b3 = SoccerBatch(N)
+    b3.reset(seed=7)
+    first = b3.obs[:, :2].clone()
+    ro = DeviceRollout(b3, agent, rms, 2, seed=9, deterministic=True, update_normalizer=False)
+    assert ro.policy == "fused"
+    out = ro.collect()
+    with torch.no_grad():
+        mean = agent.actor_mean(rms.normalize(first.reshape(-1, 66))).reshape(N, 2, 3)
+    assert float((out["actions"][0] - mean).abs().max()) <= 1e-5
+    b3.close()
 
 
 @pytest.mark.gpu
@@ -254,9 +267,13 @@ def test_bf16_policy_rollout_within_bound_and_graph_equal():
 
 
 @pytest.mark.gpu
-def test_graph_eval_matches_eager_eval():
-    """evaluate(graph=True) (one captured step replayed max_steps - 1 times) returns exactly what
-    the eager loop returns, red agents drawn from the generator included."""
+@pytest.mark.parametrize("max_steps", [120, 37, 10, 1])
+def test_graph_eval_matches_eager_eval(max_steps):
+    """evaluate(graph=True) returns exactly what the eager loop returns, red agents drawn from
+    the generator included. The graph path runs the first steps eagerly, then replays a graph of
+    min(GRAPH_CHUNK, max_steps - 1) captured steps for the rest of the episode: 120 steps
+    (20 eager, 4 replays of 25), 37 (12 eager, 1 replay: not a multiple of the chunk), 10
+    (1 eager, 1 replay of 9: shorter than a chunk), 1 (eager only: nothing is captured)."""
     if not torch.cuda.is_available():
         pytest.skip("needs a HIP device")
     from marlsoccer.config import load_config
@@ -265,12 +282,12 @@ def test_graph_eval_matches_eager_eval():
     agent = Agent().cuda()
     rms = RunningMeanStd(device="cuda")
     cfg = load_config()
-    cfg["simulation"]["max_steps"] = 120
+    cfg["simulation"]["max_steps"] = max_steps
     eager = evaluate(agent, rms, 96, seed=5, config=cfg, generator_seed=3)
     graph = evaluate(agent, rms, 96, seed=5, config=cfg, generator_seed=3, graph=True)
     np.testing.assert_array_equal(graph["returns"], eager["returns"])
     np.testing.assert_array_equal(graph["score"], eager["score"])
-    assert graph["steps"] == eager["steps"] == 120
+    assert graph["steps"] == eager["steps"] == max_steps
     with pytest.raises(ValueError):
         evaluate(agent, rms, 4, config=cfg, graph=True, frames_every=10)
 

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="DeviceRollout(graph=True): time a replay of the captured rollout graph")
     ap.add_argument("--bf16", action="store_true", help="DeviceRollout(policy_dtype=torch.bfloat16) (opt-in)")
+    ap.add_argument("--policy", choices=("fused", "torch"), default=None,
+                    help="DeviceRollout(policy=...): the fused ms_policy_forward kernel (fp32 default) or torch")
     a = ap.parse_args()
     import torch
     from marlsoccer import SoccerBatch
@@ -44,7 +46,7 @@ def main():
     warm.collect()
     if a.graph:
         ro = DeviceRollout(b, agent, rms, a.steps, seed=2, graph=True,
-                           policy_dtype=torch.bfloat16 if a.bf16 else torch.float32)
+                           policy_dtype=torch.bfloat16 if a.bf16 else torch.float32, policy=a.policy)
         ro.collect()  # eager
         ro.collect()  # capture + first replay
         torch.cuda.synchronize()
@@ -57,12 +59,13 @@ def main():
             "value": a.envs * a.steps / dt, "unit": "env-steps/s", "envs": a.envs, "steps": a.steps,
             "ms_per_step": dt * 1e3 / a.steps,
             "policy": "Agent 66-512-256-128-64-{3,1} tanh x2, " + ("bf16 autocast GEMMs" if a.bf16 else "fp32")
-                      + ", sampled actions; red uniform(-1,1)",
+                      + f" ({ro.policy}), sampled actions; red uniform(-1,1)",
             "timed": "third collect(): a replay of the graph captured by the second (normaliser update included)",
         }))
         b.close()
         return
-    ro = DeviceRollout(b, agent, rms, a.steps, seed=2, policy_dtype=torch.bfloat16 if a.bf16 else torch.float32)
+    ro = DeviceRollout(b, agent, rms, a.steps, seed=2, policy_dtype=torch.bfloat16 if a.bf16 else torch.float32,
+                       policy=a.policy)
     # env-kernel share: events around every ms_step of the timed rollout
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     step_into = b.step_into
@@ -84,7 +87,7 @@ def main():
         "metric": "rollout env-steps/s (policy + env on device)", "value": a.envs * a.steps / dt,
         "unit": "env-steps/s", "envs": a.envs, "steps": a.steps, "ms_per_step": dt * 1e3 / a.steps,
         "env_kernel_ms_per_step": env_ms / a.steps, "env_share": env_ms / (dt * 1e3),
-        "policy": "Agent 66-512-256-128-64-{3,1} tanh x2, fp32, sampled actions; red uniform(-1,1)",
+        "policy": f"Agent 66-512-256-128-64-{{3,1}} tanh x2, fp32 ({ro.policy}), sampled actions; red uniform(-1,1)",
         "reference_host_rollout_env_steps_per_s": "≈930-1430 (SURVEY.md §6, training-inclusive)",
     }))
     b.close()
