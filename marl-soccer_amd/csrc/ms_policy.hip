@@ -16,7 +16,9 @@
 //     order (marlsoccer/policy.py packs them);
 //   * weights stream from L2 (both nets are 1.7 MB, resident) as one coalesced 16-B load per
 //     lane per four MFMAs, issued a group ahead of their use;
-//   * bias and tanh are applied to the accumulator registers in place.
+//   * the accumulators start at the bias; each chunk's tanh is applied to its accumulator
+//     registers in place, interleaved with the MFMAs of the next chunk (or of the next layer's
+//     first k-steps, which read earlier tiles): VALU work under the matrix pipe's 64 cycles.
 //
 // Layer geometry (T = 32-feature output tiles, G = groups of four k-steps of two features):
 //   L1 66 -> 512 (T 16, G 9: 33 k-steps + 3 zero steps), L2 512 -> 256 (T 8, G 64),
@@ -71,19 +73,45 @@ __device__ __forceinline__ float tanh_fast(float x) {
   return __builtin_copysignf(t, x);
 }
 
-// One dense layer C^T = W . H^T (+ bias, tanh unless LAST) for T_OUT output tiles, CH tiles at
-// a time. bop(s) gives this lane's B operand of k-step s (compile-time s); W/b the layer's
-// packed weights and biases.
-template <int T_OUT, int G, int CH, bool LAST, typename BOP>
-__device__ __forceinline__ void dense(BOP&& bop, f32x16 (&Y)[T_OUT], const float* __restrict__ W,
+// One dense layer C^T = W . H^T + bias for T_OUT output tiles, CH tiles at a time. The
+// accumulators start at the bias (so the epilogue is the tanh alone), and the tanh of a chunk
+// is software-pipelined into the MFMA stream: chunk c's tanh runs one element at a time between
+// the MFMAs of chunk c + 1 (they are independent), and the last chunk's tanh is handed back as
+// `pending` work that the next layer interleaves with its first k-steps (which read earlier
+// tiles only). prev(s) is the previous layer's pending work for this layer's k-step s
+// (chunk 0); bop(s) this lane's B operand of k-step s; W/b the packed weights and biases.
+template <int T_OUT, int BASE, int CH>
+struct Pending {  // the tanh of tiles [BASE, BASE + CH) of Y, to be spread over k-steps
+  f32x16 (&Y)[T_OUT];
+  template <int S, int SPAN>
+  __device__ __forceinline__ void step() {  // element share of step S of SPAN steps
+    constexpr int E = CH * 16;
+    constexpr int lo = S * E / SPAN, hi = (S + 1) * E / SPAN;
+    static_for<lo, hi>([&](auto ec) __attribute__((always_inline)) {
+      constexpr int e = decltype(ec)::value;
+      Y[BASE + e / 16][e % 16] = tanh_fast(Y[BASE + e / 16][e % 16]);
+    });
+  }
+};
+struct NoPending {
+  template <int S, int SPAN>
+  __device__ __forceinline__ void step() {}
+};
+
+template <int T_OUT, int G, int CH, bool LAST, int SLACK, typename BOP, typename PREV>
+__device__ __forceinline__ void dense(BOP&& bop, PREV& prev, f32x16 (&Y)[T_OUT], const float* __restrict__ W,
                                       const float* __restrict__ b, int lane) {
   const int h = lane >> 5;
+  constexpr int S = 4 * G;  // k-steps
   static_for<0, T_OUT / CH>([&](auto cc) __attribute__((always_inline)) {
     constexpr int c = decltype(cc)::value;
     f32x16 acc[CH];
     static_for<0, CH>([&](auto tc) __attribute__((always_inline)) {
-      acc[decltype(tc)::value] = f32x16{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
-                                        0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+      constexpr int t = decltype(tc)::value;
+      const f32x4* bb = (const f32x4*)(b + ((c * CH + t) * 2 + h) * 16);
+      const f32x4 b0 = bb[0], b1 = bb[1], b2 = bb[2], b3 = bb[3];
+      acc[t] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                      b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
     });
     // A operands of the current group and the next DEPTH - 1 groups (a ring: each group's
     // 16-B loads are issued DEPTH - 1 groups, 4 (DEPTH - 1) CH MFMAs, ahead of their use)
@@ -107,57 +135,73 @@ __device__ __forceinline__ void dense(BOP&& bop, f32x16 (&Y)[T_OUT], const float
       }
       static_for<0, 4>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
-        const float bv = bop(std::integral_constant<int, 4 * g + j>{});
+        constexpr int s = 4 * g + j;
+        const float bv = bop(std::integral_constant<int, s>{});
         static_for<0, CH>([&](auto tc) __attribute__((always_inline)) {
           constexpr int t = decltype(tc)::value;
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g % DEPTH][t][j], bv, acc[t], 0, 0, 0);
         });
+        // interleaved VALU work: the previous layer's pending tanh (chunk 0, within the k-steps
+        // that do not read it yet) or this layer's previous chunk's tanh
+        if constexpr (c == 0) {
+          if constexpr (s < SLACK) prev.template step<s, SLACK>();
+        } else if constexpr (!LAST) {
+          Pending<T_OUT, (c - 1) * CH, CH>{Y}.template step<s, S>();
+        }
       });
     });
+    if constexpr (c == 0 && SLACK > S) {  // a chunk shorter than the slack: finish the rest
+      static_for<S, SLACK>([&](auto sc) __attribute__((always_inline)) {
+        prev.template step<decltype(sc)::value, SLACK>();
+      });
+    }
     static_for<0, CH>([&](auto tc) __attribute__((always_inline)) {
       constexpr int t = decltype(tc)::value;
-      const f32x4* bb = (const f32x4*)(b + ((c * CH + t) * 2 + h) * 16);
-      f32x16 y = acc[t];
-      static_for<0, 4>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        const f32x4 bq = bb[q];
-        static_for<0, 4>([&](auto ec) __attribute__((always_inline)) {
-          constexpr int e = decltype(ec)::value;
-          const float v = y[4 * q + e] + bq[e];
-          y[4 * q + e] = LAST ? v : tanh_fast(v);
-        });
-      });
-      Y[c * CH + t] = y;
+      Y[c * CH + t] = acc[t];
     });
   });
 }
 
 // One net (actor or critic) on the normalised inputs xk (k-step s of layer 1: feature 2s + h,
 // s < 36; steps 33-35 are zero). Returns the last layer's tile (rows 0..NOUT-1 of lane half 0).
+// The SLACK of a layer: the k-steps before it first reads the previous layer's last chunk
+// (16 (T_prev - CH_prev)); a previous layer with a single chunk gets its tanh done up front.
 __device__ __forceinline__ f32x16 net_forward(const float (&xk)[36], const float* __restrict__ P, int lane) {
+  NoPending none;
   f32x16 H1[T1];
-  dense<T1, G1, CH, false>([&](auto s) __attribute__((always_inline)) { return xk[decltype(s)::value]; }, H1, P + OW1,
-                          P + OB1, lane);
+  dense<T1, G1, CH, false, 0>([&](auto s) __attribute__((always_inline)) { return xk[decltype(s)::value]; }, none, H1,
+                              P + OW1, P + OB1, lane);
+  Pending<T1, T1 - CH, CH> p1{H1};
   f32x16 H2[T2];
-  dense<T2, G2, CH, false>([&](auto s) __attribute__((always_inline)) {
+  dense<T2, G2, CH, false, 16 * (T1 - CH)>([&](auto s) __attribute__((always_inline)) {
     constexpr int k = decltype(s)::value;
     return H1[k >> 4][k & 15];
-  }, H2, P + OW2, P + OB2, lane);
+  }, p1, H2, P + OW2, P + OB2, lane);
+  Pending<T2, T2 - CH, CH> p2{H2};
   f32x16 H3[T3];
-  dense<T3, G3, CH, false>([&](auto s) __attribute__((always_inline)) {
+  dense<T3, G3, CH, false, 16 * (T2 - CH)>([&](auto s) __attribute__((always_inline)) {
     constexpr int k = decltype(s)::value;
     return H2[k >> 4][k & 15];
-  }, H3, P + OW3, P + OB3, lane);
+  }, p2, H3, P + OW3, P + OB3, lane);
+  // layer 3 is one chunk (T3 = CH): its tanh before layer 4, which reads it from k-step 0
+  static_for<0, T3 * 16>([&](auto ec) __attribute__((always_inline)) {
+    constexpr int e = decltype(ec)::value;
+    H3[e / 16][e % 16] = tanh_fast(H3[e / 16][e % 16]);
+  });
   f32x16 H4[T4];
-  dense<T4, G4, 2, false>([&](auto s) __attribute__((always_inline)) {
+  dense<T4, G4, 2, false, 0>([&](auto s) __attribute__((always_inline)) {
     constexpr int k = decltype(s)::value;
     return H3[k >> 4][k & 15];
-  }, H4, P + OW4, P + OB4, lane);
+  }, none, H4, P + OW4, P + OB4, lane);
+  static_for<0, T4 * 16>([&](auto ec) __attribute__((always_inline)) {
+    constexpr int e = decltype(ec)::value;
+    H4[e / 16][e % 16] = tanh_fast(H4[e / 16][e % 16]);
+  });
   f32x16 H5[T5];
-  dense<T5, G5, 1, true>([&](auto s) __attribute__((always_inline)) {
+  dense<T5, G5, 1, true, 0>([&](auto s) __attribute__((always_inline)) {
     constexpr int k = decltype(s)::value;
     return H4[k >> 4][k & 15];
-  }, H5, P + OW5, P + OB5, lane);
+  }, none, H5, P + OW5, P + OB5, lane);
   return H5[0];
 }
 
