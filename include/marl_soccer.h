@@ -282,6 +282,28 @@ int ms_policy_forward(const float *x, int64_t rows, int group_rows, int64_t grou
                       float *act_mean, float *value, void *stream);
 const char *ms_policy_last_error(void);
 
+/* The same kernel with every output of one rollout step (marlsoccer.rollout.DeviceRollout;
+ * the notebook's rollout L299-313): NULL pointers are not written. Row r as above; outputs
+ * per row: act_mean [rows][3], value [rows]; action [rows][3] = eps * exp(logstd) + mean when
+ * eps (device standard-normal draws [rows][3]) is given (Agent.sample), else the mean;
+ * logprob [rows] = its Normal log-prob summed over the 3 components (0 without eps);
+ * obs_copy [rows][66] the raw input rows; env_actions [rows / 2][4][3]: row r's action at
+ * env r / 2, agent r % 2 (the blue agents of the env's action buffer; rows even), and with
+ * red_uniform (device uniform [0, 1) draws [rows][3]) 2u - 1 at env r / 2, agent 2 + r % 2. */
+typedef struct ms_policy_io {
+  const float *obs;
+  int64_t rows;
+  int32_t group_rows;
+  int32_t pad0;
+  int64_t group_stride, row_stride;
+  const double *mean, *den;
+  const float *actor, *critic;
+  const float *logstd, *eps;
+  float *act_mean, *action, *logprob, *value, *obs_copy, *env_actions;
+  const float *red_uniform;
+} ms_policy_io;
+int ms_policy_run(const ms_policy_io *io, void *stream);
+
 /* Synchronises the stream and reads the device counters. */
 int ms_get_stats(ms_env *env, ms_stats *out);
 int ms_reset_stats(ms_env *env);

@@ -205,20 +205,16 @@ __device__ __forceinline__ f32x16 net_forward(const float (&xk)[36], const float
   return H5[0];
 }
 
-// Row r of the input: x + (r / group_rows) * group_stride + (r % group_rows) * row_stride.
-__global__ __launch_bounds__(64) void policy_forward_kernel(const float* __restrict__ x, int64_t rows, int group_rows,
-                                                            int64_t group_stride, int64_t row_stride,
-                                                            const double* __restrict__ mean,
-                                                            const double* __restrict__ den,
-                                                            const float* __restrict__ actor,
-                                                            const float* __restrict__ critic,
-                                                            float* __restrict__ act_mean, float* __restrict__ value) {
+// Row r of the input: obs + (r / group_rows) * group_stride + (r % group_rows) * row_stride.
+// One launch per rollout step (ms_policy_run, include/marl_soccer.h): NULL outputs are skipped
+// (wave-uniform branches).
+__global__ __launch_bounds__(64) void policy_kernel(const ms_policy_io io) {
   const int lane = threadIdx.x;
   const int h = lane >> 5;
   const int64_t row = (int64_t)blockIdx.x * TM + (lane & 31);
-  const bool valid = row < rows;
-  const int64_t rr = valid ? row : rows - 1;
-  const float* xr = x + (rr / group_rows) * group_stride + (rr % group_rows) * row_stride;
+  const bool valid = row < io.rows;
+  const int64_t rr = valid ? row : io.rows - 1;
+  const float* xr = io.obs + (rr / io.group_rows) * io.group_stride + (rr % io.group_rows) * io.row_stride;
   // layer-1 B operand: feature 2s + h of this lane's row, normalised as RunningMeanStd.normalize
   // (float64 (x - mean) / (sqrt(var) + 1e-8), clip to [-10, 10], float32)
   float xk[36];
@@ -226,8 +222,9 @@ __global__ __launch_bounds__(64) void policy_forward_kernel(const float* __restr
   for (int s = 0; s < 33; ++s) {
     const int f = 2 * s + h;
     const float v = xr[f];
-    if (mean) {
-      double y = ((double)v - mean[f]) / den[f];
+    if (io.obs_copy && valid) io.obs_copy[row * 66 + f] = v;  // the rollout's obs storage (raw)
+    if (io.mean) {
+      double y = ((double)v - io.mean[f]) / io.den[f];
       y = y < -10.0 ? -10.0 : (y > 10.0 ? 10.0 : y);
       xk[s] = (float)y;
     } else {
@@ -235,17 +232,33 @@ __global__ __launch_bounds__(64) void policy_forward_kernel(const float* __restr
     }
   }
   xk[33] = 0.0f; xk[34] = 0.0f; xk[35] = 0.0f;
-  if (actor) {
-    const f32x16 m = net_forward(xk, actor, lane);
+  if (io.actor) {
+    const f32x16 m = net_forward(xk, io.actor, lane);
     if (valid && h == 0) {  // rows 0..2 of the tile = the three action components, lane half 0
-      act_mean[row * 3 + 0] = m[0];
-      act_mean[row * 3 + 1] = m[1];
-      act_mean[row * 3 + 2] = m[2];
+      float act[3];
+      float lp = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        if (io.act_mean) io.act_mean[row * 3 + c] = m[c];
+        act[c] = m[c];
+        if (io.eps) {  // Agent.sample: eps * exp(logstd) + mean; Normal(mean, std).log_prob summed
+          const float ls = io.logstd[c];
+          const float sd = expf(ls);
+          act[c] = io.eps[row * 3 + c] * sd + m[c];
+          const float d = act[c] - m[c];
+          lp += -(d * d) / (2.0f * (sd * sd)) - ls - 0.91893853320467274f;  // log sqrt(2 pi)
+        }
+        if (io.action) io.action[row * 3 + c] = act[c];
+        if (io.env_actions) io.env_actions[((row >> 1) * 4 + (row & 1)) * 3 + c] = act[c];
+        if (io.env_actions && io.red_uniform)
+          io.env_actions[((row >> 1) * 4 + 2 + (row & 1)) * 3 + c] = io.red_uniform[row * 3 + c] * 2.0f - 1.0f;
+      }
+      if (io.logprob) io.logprob[row] = lp;
     }
   }
-  if (critic) {
-    const f32x16 v = net_forward(xk, critic, lane);
-    if (valid && h == 0) value[row] = v[0];
+  if (io.critic) {
+    const f32x16 v = net_forward(xk, io.critic, lane);
+    if (valid && h == 0 && io.value) io.value[row] = v[0];
   }
 }
 
@@ -256,6 +269,17 @@ static thread_local std::string g_pol_err;
 extern "C" {
 
 const char* ms_policy_last_error(void) { return g_pol_err.c_str(); }
+
+static int launch(const ms_policy_io& io, void* stream, const char* who) {
+  const unsigned grid = (unsigned)((io.rows + pol::TM - 1) / pol::TM);
+  hipLaunchKernelGGL(pol::policy_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, io);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_pol_err = std::string(who) + ": " + hipGetErrorString(e);
+    return MS_ERR_HIP;
+  }
+  return MS_OK;
+}
 
 int ms_policy_forward(const float* x, int64_t rows, int group_rows, int64_t group_stride, int64_t row_stride,
                       const double* mean, const double* den, const float* actor, const float* critic, float* act_mean,
@@ -269,15 +293,25 @@ int ms_policy_forward(const float* x, int64_t rows, int group_rows, int64_t grou
     g_pol_err = "ms_policy_forward: packed weights must be 16-B aligned";
     return MS_ERR_INVALID_ARGUMENT;
   }
-  const unsigned grid = (unsigned)((rows + pol::TM - 1) / pol::TM);
-  hipLaunchKernelGGL(pol::policy_forward_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, x, rows, group_rows,
-                     group_stride, row_stride, mean, den, actor, critic, act_mean, value);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    g_pol_err = std::string("ms_policy_forward: ") + hipGetErrorString(e);
-    return MS_ERR_HIP;
+  ms_policy_io io = {};
+  io.obs = x; io.rows = rows; io.group_rows = group_rows; io.group_stride = group_stride; io.row_stride = row_stride;
+  io.mean = mean; io.den = den; io.actor = actor; io.critic = critic; io.act_mean = act_mean; io.value = value;
+  return launch(io, stream, "ms_policy_forward");
+}
+
+int ms_policy_run(const ms_policy_io* io, void* stream) {
+  if (!io || !io->obs || io->rows <= 0 || io->group_rows <= 0 || (!io->actor && !io->critic) ||
+      (!io->mean) != (!io->den) || (io->eps && !io->logstd) || (io->eps && !io->actor) ||
+      (io->env_actions && (!io->actor || (io->rows & 1))) || (io->red_uniform && !io->env_actions) ||
+      ((io->act_mean || io->action || io->logprob || io->env_actions) && !io->actor) || (io->value && !io->critic)) {
+    g_pol_err = "ms_policy_run: bad arguments";
+    return MS_ERR_INVALID_ARGUMENT;
   }
-  return MS_OK;
+  if (((uintptr_t)io->actor & 15u) || ((uintptr_t)io->critic & 15u)) {
+    g_pol_err = "ms_policy_run: packed weights must be 16-B aligned";
+    return MS_ERR_INVALID_ARGUMENT;
+  }
+  return launch(*io, stream, "ms_policy_run");
 }
 
 }  // extern "C"

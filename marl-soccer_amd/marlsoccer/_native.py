@@ -45,6 +45,15 @@ class MsStats(C.Structure):
                 ("cache_entries_written", C.c_uint64)]
 
 
+class MsPolicyIO(C.Structure):
+    """ms_policy_io (include/marl_soccer.h): device pointers of one policy-kernel launch."""
+    _fields_ = [("obs", C.c_void_p), ("rows", C.c_int64), ("group_rows", C.c_int32), ("pad0", C.c_int32),
+                ("group_stride", C.c_int64), ("row_stride", C.c_int64), ("mean", C.c_void_p), ("den", C.c_void_p),
+                ("actor", C.c_void_p), ("critic", C.c_void_p), ("logstd", C.c_void_p), ("eps", C.c_void_p),
+                ("act_mean", C.c_void_p), ("action", C.c_void_p), ("logprob", C.c_void_p), ("value", C.c_void_p),
+                ("obs_copy", C.c_void_p), ("env_actions", C.c_void_p), ("red_uniform", C.c_void_p)]
+
+
 # numpy view of ms_env_state (include/marl_soccer.h), for export/import
 BODY_DTYPE = np.dtype([(n, "<f4") for n in ("px", "py", "vx", "vy", "angle", "w", "vbx", "vby", "wb")])
 ARB_DTYPE = np.dtype([("pair", "u1"), ("count", "u1"), ("idle", "u1"), ("pad0", "u1"),
@@ -63,7 +72,7 @@ EXPORTED = (
     "ms_seed_pcg64_range", "ms_reset", "ms_step", "ms_observe", "ms_export_state", "ms_import_state",
     "ms_debug_rewards", "ms_get_stats", "ms_reset_stats", "ms_last_error", "ms_abi_version",
     "ms_config_specialised", "ms_step_ring", "ms_reset_ring", "ms_set_persistent", "ms_get_persistent",
-    "ms_policy_forward", "ms_policy_last_error",
+    "ms_policy_forward", "ms_policy_last_error", "ms_policy_run",
 )
 
 _lib = None
@@ -124,6 +133,8 @@ def lib():
         L.ms_policy_forward.argtypes = [P, I64, C.c_int, I64, I64, P, P, P, P, P, P, P]
         L.ms_policy_forward.restype = C.c_int
         L.ms_policy_last_error.restype = C.c_char_p
+        L.ms_policy_run.argtypes = [C.POINTER(MsPolicyIO), P]
+        L.ms_policy_run.restype = C.c_int
     for fn in ("ms_create", "ms_destroy", "ms_set_stream", "ms_seed_pcg64", "ms_seed_pcg64_range", "ms_reset",
                "ms_step", "ms_observe", "ms_export_state", "ms_import_state", "ms_debug_rewards",
                "ms_get_stats", "ms_reset_stats"):

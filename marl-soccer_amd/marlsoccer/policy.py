@@ -126,3 +126,33 @@ class FusedPolicy:
             raise (ValueError if rc == N.MS_ERR_INVALID_ARGUMENT else N.NativeError)(
                 self._L.ms_policy_last_error().decode(errors="replace"))
         return act_mean, value
+
+    def run(self, obs: torch.Tensor, rows: int, group_rows: int, group_stride: int, row_stride: int = 66,
+            mean: torch.Tensor | None = None, den: torch.Tensor | None = None, eps: torch.Tensor | None = None,
+            act_mean=None, action=None, logprob=None, value=None, obs_copy=None, env_actions=None,
+            red_uniform: torch.Tensor | None = None) -> None:
+        """ms_policy_run: one launch with every output of a rollout step (include/marl_soccer.h);
+        the output tensors are written in place (None: not written). eps: standard-normal draws
+        (rows, 3) for sampled actions (Agent.sample with the agent's actor_logstd), or None for the
+        deterministic mean. red_uniform: uniform [0, 1) draws (rows, 3) written as 2u - 1 into the
+        red agents' rows of env_actions."""
+        dev = self.packed.device
+        for t in (obs, mean, den, eps, act_mean, action, logprob, value, obs_copy, env_actions, red_uniform):
+            if t is not None and (t.device != dev or not t.is_contiguous()):
+                raise ValueError("ms_policy_run: tensors must be contiguous on the policy's device")
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        io = N.MsPolicyIO(obs=p(obs), rows=int(rows), group_rows=int(group_rows), pad0=0, group_stride=int(group_stride),
+                          row_stride=int(row_stride), mean=p(mean), den=p(den), actor=self.packed[0].data_ptr(),
+                          critic=self.packed[1].data_ptr(),
+                          logstd=None if eps is None else self.logstd.data_ptr(), eps=p(eps),
+                          act_mean=p(act_mean), action=p(action), logprob=p(logprob), value=p(value),
+                          obs_copy=p(obs_copy), env_actions=p(env_actions), red_uniform=p(red_uniform))
+        rc = self._L.ms_policy_run(C.byref(io), C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+        if rc:
+            raise (ValueError if rc == N.MS_ERR_INVALID_ARGUMENT else N.NativeError)(
+                self._L.ms_policy_last_error().decode(errors="replace"))
+
+    @property
+    def logstd(self) -> torch.Tensor:
+        """The agent's actor_logstd (1, 3) float32, contiguous (read in place)."""
+        return self.agent.actor_logstd

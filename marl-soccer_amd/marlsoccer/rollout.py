@@ -177,8 +177,6 @@ class DeviceRollout:
         if policy == "fused":
             from .policy import FusedPolicy
             self._fused = FusedPolicy(agent)
-            self._am = torch.zeros((batch.num_envs * 2, ACT_DIM), dtype=torch.float32, device=batch.device)
-            self._val = torch.zeros((batch.num_envs * 2,), dtype=torch.float32, device=batch.device)
             self._den = torch.ones((OBS_DIM,), dtype=torch.float64, device=batch.device)
         self._graph = None
         self._graph_inputs = None
@@ -202,15 +200,26 @@ class DeviceRollout:
     @torch.no_grad()
     def step(self, t: int) -> None:
         b = self.batch
-        self.obs[t] = self.next_obs
         self.dones[t] = self.next_done
+        if self._fused is None:
+            self.obs[t] = self.next_obs
         if self._fused is not None:
-            # normalisation + actor + critic in one kernel, straight from the (N, 2, 66) obs rows
-            self._fused.forward(self.next_obs, self.normalizer.mean, self._den, act_mean=self._am, value=self._val)
-            action_mean, value = self._am, self._val
-            if self.deterministic:
-                action = action_mean
-                logprob = torch.zeros(action_mean.shape[0], device=action_mean.device)
+            # ONE kernel: normalisation, actor, critic, sampling and log-prob, straight from the
+            # env's (N, 4, 66) obs rows of the blue agents into the storage and the env's actions
+            # (the same generator draws as the torch path: eps, then the red agents' uniforms)
+            eps = None if self.deterministic else torch.randn((2 * self.N, ACT_DIM), device=b.device, generator=self.gen)
+            red = torch.rand((2 * self.N, ACT_DIM), generator=self.gen, device=b.device)
+            self._fused.run(b.obs, 2 * self.N, 2, 264, 66, self.normalizer.mean, self._den, eps=eps,
+                            action=self.actions[t], logprob=self.logprobs[t], value=self.values[t],
+                            obs_copy=self.obs[t], env_actions=self.full_actions, red_uniform=red)
+            b.step_into(self.full_actions, b.obs, b.rew, b.term, b.trunc, b.goal, b.score)
+            self.rewards[t] = b.rew[:, :2]
+            done = (b.term[:, :2] | b.trunc[:, :2]).to(torch.float32)
+            self.next_done.copy_(done)
+            finished = b.trunc[:, 0].to(torch.bool)
+            self.episodes += finished.sum()
+            self.score_sum += (b.score * finished[:, None]).sum(dim=0)
+            return
         else:
             x = self.normalizer.normalize(self.next_obs.reshape(-1, OBS_DIM))
             # no autocast weight-cast cache: its casts would be allocated and reused across a graph
@@ -248,6 +257,8 @@ class DeviceRollout:
             torch.add(self.normalizer.std, 1e-8, out=self._den)
         for t in range(self.T):
             self.step(t)
+        if self._fused is not None:  # the fused step reads the env's obs rows directly
+            self.next_obs.copy_(self.batch.obs[:, :2])
 
     def _inputs_identity(self) -> tuple:
         """The tensors a captured rollout reads in place (their storage)."""

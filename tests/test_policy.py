@@ -364,3 +364,38 @@ def test_fused_policy_kernel_normalises_like_running_mean_std():
                 p.add_(0.01 * torch.randn_like(p))
         fp.pack()
     env.close()
+
+
+@pytest.mark.gpu
+def test_fused_rollout_step_matches_torch_policy_rollout():
+    """DeviceRollout's fused step (one ms_policy_run launch: normalisation, both MLPs, sampling,
+    log-prob, storage and the env's blue actions) against the torch-module rollout from the same
+    state and generator seed: the first step's stored actions, log-probs and values within 1e-5
+    (same random draws: the kernel consumes eps from the same generator calls), obs and dones
+    equal."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer import SoccerBatch
+    N, T = 512, 1
+    torch.manual_seed(0)
+    agent = Agent().cuda()
+    with torch.no_grad():
+        agent.actor_logstd.copy_(torch.tensor([[-0.3, 0.1, 0.4]]))
+    rms = RunningMeanStd((66,), device="cuda")
+    rms.mean.copy_(torch.from_numpy(FX["run5_mean"]))
+    rms.var.copy_(torch.from_numpy(FX["run5_var"]))
+    outs = {}
+    for pol in ("torch", "fused"):
+        b = SoccerBatch(N)
+        b.reset(seed=41)
+        ro = DeviceRollout(b, agent, rms, T, seed=6, update_normalizer=False, policy=pol)
+        assert ro.policy == pol
+        outs[pol] = {k: v.clone() for k, v in ro.collect().items()}
+        outs[pol]["full_actions"] = ro.full_actions.clone()
+        b.close()
+    a, f = outs["torch"], outs["fused"]
+    assert torch.equal(a["obs"], f["obs"]) and torch.equal(a["dones"], f["dones"])
+    for k in ("actions", "logprobs", "values"):
+        assert float((a[k] - f[k]).abs().max()) <= 1e-5, k
+    assert torch.equal(f["full_actions"][:, :2], f["actions"][0])
+    assert torch.equal(a["full_actions"][:, 2:], f["full_actions"][:, 2:])  # the same red draws
