@@ -304,6 +304,16 @@ typedef struct ms_policy_io {
 } ms_policy_io;
 int ms_policy_run(const ms_policy_io *io, void *stream);
 
+/* A rollout step's bookkeeping from ms_step's outputs in one launch (marlsoccer.rollout.
+ * DeviceRollout; the notebook's rollout L313-336, PPO storage of the two blue agents): for env
+ * i < n_envs and agent a < 2, rewards[i][a] = rew[i][a] and next_done[i][a] = 1.0f if
+ * term[i][a] | trunc[i][a] else 0.0f (also into dones_next[i][a] when non-NULL: the next
+ * step's row of the dones storage); every env with trunc[i][0] adds 1 to *episodes and
+ * score[i][0..1] to score_sum[0..1] (int64, device). All pointers device memory. */
+int ms_rollout_record(int64_t n_envs, const float *rew, const uint8_t *term, const uint8_t *trunc,
+                      const int32_t *score, float *rewards, float *next_done, float *dones_next,
+                      int64_t *episodes, int64_t *score_sum, void *stream);
+
 /* Synchronises the stream and reads the device counters. */
 int ms_get_stats(ms_env *env, ms_stats *out);
 int ms_reset_stats(ms_env *env);

@@ -215,6 +215,21 @@ __global__ __launch_bounds__(64) void policy_kernel(const ms_policy_io io) {
   const bool valid = row < io.rows;
   const int64_t rr = valid ? row : io.rows - 1;
   const float* xr = io.obs + (rr / io.group_rows) * io.group_stride + (rr % io.group_rows) * io.row_stride;
+  // the rollout's obs storage: the tile's rows as 8-B pieces, lanes over consecutive pieces of
+  // the contiguous destination (a row's 66 features are contiguous in the source as well)
+  const bool copy_pairs = io.obs_copy && !(((uintptr_t)io.obs | (uintptr_t)io.obs_copy) & 7u) &&
+                          !((io.row_stride | io.group_stride) & 1);
+  if (copy_pairs) {
+    const int64_t row0 = (int64_t)blockIdx.x * TM;
+    const int nr = (int)(io.rows - row0 < TM ? io.rows - row0 : TM);
+    for (int i = lane; i < nr * 33; i += 64) {
+      const int r = i / 33, c = i - 33 * r;
+      const int64_t q = row0 + r;
+      const float2 v = *(const float2*)(io.obs + (q / io.group_rows) * io.group_stride +
+                                        (q % io.group_rows) * io.row_stride + 2 * c);
+      *(float2*)(io.obs_copy + q * 66 + 2 * c) = v;
+    }
+  }
   // layer-1 B operand: feature 2s + h of this lane's row, normalised as RunningMeanStd.normalize
   // (float64 (x - mean) / (sqrt(var) + 1e-8), clip to [-10, 10], float32)
   float xk[36];
@@ -222,7 +237,7 @@ __global__ __launch_bounds__(64) void policy_kernel(const ms_policy_io io) {
   for (int s = 0; s < 33; ++s) {
     const int f = 2 * s + h;
     const float v = xr[f];
-    if (io.obs_copy && valid) io.obs_copy[row * 66 + f] = v;  // the rollout's obs storage (raw)
+    if (io.obs_copy && !copy_pairs && valid) io.obs_copy[row * 66 + f] = v;  // unaligned fallback
     if (io.mean) {
       double y = ((double)v - io.mean[f]) / io.den[f];
       y = y < -10.0 ? -10.0 : (y > 10.0 ? 10.0 : y);
@@ -259,6 +274,44 @@ __global__ __launch_bounds__(64) void policy_kernel(const ms_policy_io io) {
   if (io.critic) {
     const f32x16 v = net_forward(xk, io.critic, lane);
     if (valid && h == 0 && io.value) io.value[row] = v[0];
+  }
+}
+
+// ms_rollout_record: one env per lane; the finished-episode count and scores reduced per wave
+// (cross-lane adds), one device atomic per wave and counter.
+__global__ __launch_bounds__(256) void rollout_record_kernel(int64_t n, const float* __restrict__ rew,
+                                                             const uint8_t* __restrict__ term,
+                                                             const uint8_t* __restrict__ trunc,
+                                                             const int32_t* __restrict__ score,
+                                                             float* __restrict__ rewards, float* __restrict__ next_done,
+                                                             float* __restrict__ dones_next, int64_t* episodes,
+                                                             int64_t* score_sum) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int fin = 0, sb = 0, sr = 0;
+  if (i < n) {
+    const float2 r = *(const float2*)(rew + i * 4);
+    *(float2*)(rewards + i * 2) = r;
+    const uint32_t te = *(const uint32_t*)(term + i * 4), tr = *(const uint32_t*)(trunc + i * 4);
+    const uint32_t d = te | tr;
+    const float2 dn = make_float2((d & 0xffu) ? 1.0f : 0.0f, (d & 0xff00u) ? 1.0f : 0.0f);
+    *(float2*)(next_done + i * 2) = dn;
+    if (dones_next) *(float2*)(dones_next + i * 2) = dn;
+    if (tr & 0xffu) {
+      fin = 1;
+      sb = score[i * 2];
+      sr = score[i * 2 + 1];
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    fin += __shfl_xor(fin, m);
+    sb += __shfl_xor(sb, m);
+    sr += __shfl_xor(sr, m);
+  }
+  if ((threadIdx.x & 63) == 0 && fin) {
+    atomicAdd((unsigned long long*)episodes, (unsigned long long)fin);
+    atomicAdd((unsigned long long*)score_sum, (unsigned long long)(int64_t)sb);
+    atomicAdd((unsigned long long*)(score_sum + 1), (unsigned long long)(int64_t)sr);
   }
 }
 
@@ -312,6 +365,27 @@ int ms_policy_run(const ms_policy_io* io, void* stream) {
     return MS_ERR_INVALID_ARGUMENT;
   }
   return launch(*io, stream, "ms_policy_run");
+}
+
+int ms_rollout_record(int64_t n_envs, const float* rew, const uint8_t* term, const uint8_t* trunc,
+                      const int32_t* score, float* rewards, float* next_done, float* dones_next, int64_t* episodes,
+                      int64_t* score_sum, void* stream) {
+  if (n_envs <= 0 || !rew || !term || !trunc || !score || !rewards || !next_done || !episodes || !score_sum ||
+      (((uintptr_t)rew | (uintptr_t)rewards | (uintptr_t)next_done | (uintptr_t)dones_next | (uintptr_t)episodes |
+        (uintptr_t)score_sum) & 7u) ||
+      (((uintptr_t)term | (uintptr_t)trunc | (uintptr_t)score) & 3u)) {
+    g_pol_err = "ms_rollout_record: bad arguments (NULL or misaligned pointers)";
+    return MS_ERR_INVALID_ARGUMENT;
+  }
+  const unsigned grid = (unsigned)((n_envs + 255) / 256);
+  hipLaunchKernelGGL(pol::rollout_record_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_envs, rew, term,
+                     trunc, score, rewards, next_done, dones_next, episodes, score_sum);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_pol_err = std::string("ms_rollout_record: ") + hipGetErrorString(e);
+    return MS_ERR_HIP;
+  }
+  return MS_OK;
 }
 
 }  // extern "C"

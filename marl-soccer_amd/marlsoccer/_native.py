@@ -72,7 +72,7 @@ EXPORTED = (
     "ms_seed_pcg64_range", "ms_reset", "ms_step", "ms_observe", "ms_export_state", "ms_import_state",
     "ms_debug_rewards", "ms_get_stats", "ms_reset_stats", "ms_last_error", "ms_abi_version",
     "ms_config_specialised", "ms_step_ring", "ms_reset_ring", "ms_set_persistent", "ms_get_persistent",
-    "ms_policy_forward", "ms_policy_last_error", "ms_policy_run",
+    "ms_policy_forward", "ms_policy_last_error", "ms_policy_run", "ms_rollout_record",
 )
 
 _lib = None
@@ -135,6 +135,8 @@ def lib():
         L.ms_policy_last_error.restype = C.c_char_p
         L.ms_policy_run.argtypes = [C.POINTER(MsPolicyIO), P]
         L.ms_policy_run.restype = C.c_int
+        L.ms_rollout_record.argtypes = [I64, P, P, P, P, P, P, P, P, P, P]
+        L.ms_rollout_record.restype = C.c_int
     for fn in ("ms_create", "ms_destroy", "ms_set_stream", "ms_seed_pcg64", "ms_seed_pcg64_range", "ms_reset",
                "ms_step", "ms_observe", "ms_export_state", "ms_import_state", "ms_debug_rewards",
                "ms_get_stats", "ms_reset_stats"):

@@ -156,3 +156,28 @@ class FusedPolicy:
     def logstd(self) -> torch.Tensor:
         """The agent's actor_logstd (1, 3) float32, contiguous (read in place)."""
         return self.agent.actor_logstd
+
+
+def rollout_record(rew: torch.Tensor, term: torch.Tensor, trunc: torch.Tensor, score: torch.Tensor,
+                   rewards: torch.Tensor, next_done: torch.Tensor, dones_next: torch.Tensor | None,
+                   episodes: torch.Tensor, score_sum: torch.Tensor) -> None:
+    """ms_rollout_record (include/marl_soccer.h): a rollout step's storage and episode counters
+    from ms_step's (N, 4) outputs in one launch — rewards (N, 2) = rew[:, :2], next_done (and
+    dones_next) = float(term | trunc)[:, :2], and for every env whose episode ended
+    (trunc[:, 0]) episodes += 1, score_sum += score (int64)."""
+    n = rew.shape[0]
+    shapes = ((rew, (n, 4), torch.float32), (term, (n, 4), torch.uint8), (trunc, (n, 4), torch.uint8),
+              (score, (n, 2), torch.int32), (rewards, (n, 2), torch.float32), (next_done, (n, 2), torch.float32),
+              (dones_next, (n, 2), torch.float32), (episodes, (), torch.int64), (score_sum, (2,), torch.int64))
+    for t, shape, dtype in shapes:
+        if t is None:
+            continue
+        if tuple(t.shape) != shape or t.dtype != dtype or not t.is_contiguous() or t.device != rew.device:
+            raise ValueError(f"ms_rollout_record: expected a contiguous {dtype} {shape} tensor on {rew.device}")
+    L = N.lib()
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    rc = L.ms_rollout_record(n, p(rew), p(term), p(trunc), p(score), p(rewards), p(next_done), p(dones_next),
+                             p(episodes), p(score_sum), C.c_void_p(torch.cuda.current_stream(rew.device).cuda_stream))
+    if rc:
+        raise (ValueError if rc == N.MS_ERR_INVALID_ARGUMENT else N.NativeError)(
+            L.ms_policy_last_error().decode(errors="replace"))

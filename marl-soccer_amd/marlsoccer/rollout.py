@@ -21,6 +21,8 @@ import torch
 import torch.nn as nn
 from torch.distributions.normal import Normal
 
+from .policy import rollout_record
+
 OBS_DIM, ACT_DIM = 66, 3
 TRAINABLE = (0, 1)   # agent_0, agent_1 (blue) — notebook L243
 RANDOM = (2, 3)      # red agents act uniformly at random — notebook L315-316
@@ -200,7 +202,8 @@ class DeviceRollout:
     @torch.no_grad()
     def step(self, t: int) -> None:
         b = self.batch
-        self.dones[t] = self.next_done
+        if self._fused is None or t == 0:  # the fused step's record launch writes row t + 1
+            self.dones[t] = self.next_done
         if self._fused is None:
             self.obs[t] = self.next_obs
         if self._fused is not None:
@@ -213,12 +216,9 @@ class DeviceRollout:
                             action=self.actions[t], logprob=self.logprobs[t], value=self.values[t],
                             obs_copy=self.obs[t], env_actions=self.full_actions, red_uniform=red)
             b.step_into(self.full_actions, b.obs, b.rew, b.term, b.trunc, b.goal, b.score)
-            self.rewards[t] = b.rew[:, :2]
-            done = (b.term[:, :2] | b.trunc[:, :2]).to(torch.float32)
-            self.next_done.copy_(done)
-            finished = b.trunc[:, 0].to(torch.bool)
-            self.episodes += finished.sum()
-            self.score_sum += (b.score * finished[:, None]).sum(dim=0)
+            # ONE launch for the step's rewards, dones and finished-episode counters
+            rollout_record(b.rew, b.term, b.trunc, b.score, self.rewards[t], self.next_done,
+                           self.dones[t + 1] if t + 1 < self.T else None, self.episodes, self.score_sum)
             return
         else:
             x = self.normalizer.normalize(self.next_obs.reshape(-1, OBS_DIM))

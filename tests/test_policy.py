@@ -399,3 +399,69 @@ def test_fused_rollout_step_matches_torch_policy_rollout():
         assert float((a[k] - f[k]).abs().max()) <= 1e-5, k
     assert torch.equal(f["full_actions"][:, :2], f["actions"][0])
     assert torch.equal(a["full_actions"][:, 2:], f["full_actions"][:, 2:])  # the same red draws
+
+
+@pytest.mark.gpu
+def test_rollout_record_matches_torch_bookkeeping():
+    """ms_rollout_record (one launch) == the torch ops of the torch-policy step (rewards, dones,
+    finished-episode count and scores) on random env outputs, including ragged n (not a
+    multiple of the wave) and accumulation over two calls; bad shapes raise before launching."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer.policy import rollout_record
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    for n in (1, 63, 4099):
+        episodes = torch.zeros((), dtype=torch.int64, device="cuda")
+        score_sum = torch.zeros((2,), dtype=torch.int64, device="cuda")
+        want_ep, want_sc = 0, torch.zeros(2, dtype=torch.int64, device="cuda")
+        for _ in range(2):
+            rew = torch.randn((n, 4), generator=g, device="cuda")
+            term = (torch.rand((n, 4), generator=g, device="cuda") < 0.2).to(torch.uint8)
+            trunc = (torch.rand((n, 4), generator=g, device="cuda") < 0.3).to(torch.uint8)
+            score = torch.randint(0, 7, (n, 2), generator=g, device="cuda", dtype=torch.int32)
+            rewards = torch.full((n, 2), 7.0, device="cuda")
+            next_done = torch.full((n, 2), 7.0, device="cuda")
+            dones_next = torch.full((n, 2), 7.0, device="cuda")
+            rollout_record(rew, term, trunc, score, rewards, next_done, dones_next, episodes, score_sum)
+            assert torch.equal(rewards, rew[:, :2])
+            done = (term[:, :2] | trunc[:, :2]).to(torch.float32)
+            assert torch.equal(next_done, done) and torch.equal(dones_next, done)
+            finished = trunc[:, 0].to(torch.bool)
+            want_ep += int(finished.sum())
+            want_sc += (score * finished[:, None]).sum(dim=0)
+        assert int(episodes) == want_ep and torch.equal(score_sum, want_sc)
+    with pytest.raises(ValueError):
+        rollout_record(rew, term, trunc, score.to(torch.int64), rewards, next_done, None, episodes, score_sum)
+
+
+@pytest.mark.gpu
+def test_fused_rollout_episode_bookkeeping():
+    """A fused-policy rollout across episode ends (max_steps 5, 12 steps): dones rows mark the
+    truncation steps (the step after an episode's last one starts with done = 1), every env
+    finishes two episodes, and the score sum equals the scores the env reported at those ends."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer import SoccerBatch
+    from marlsoccer.config import load_config
+    N, T = 300, 12
+    cfg = load_config()
+    cfg["simulation"]["max_steps"] = 5
+    b = SoccerBatch(N, config=cfg)
+    b.reset(seed=3)
+    torch.manual_seed(0)
+    agent = Agent().cuda()
+    rms = RunningMeanStd((66,), device="cuda")
+    ro = DeviceRollout(b, agent, rms, T, seed=2, update_normalizer=False)
+    assert ro.policy == "fused"
+    out = ro.collect()
+    torch.cuda.synchronize()
+    want = torch.zeros((T, N, 2), device="cuda")
+    want[5] = 1.0   # steps 4 and 9 end the episodes: dones of the following steps
+    want[10] = 1.0
+    assert torch.equal(out["dones"], want)
+    assert int(out["episodes"]) == 2 * N
+    assert torch.equal(out["next_done"], torch.zeros((N, 2), device="cuda"))
+    assert torch.isfinite(out["rewards"]).all() and float(out["rewards"].abs().sum()) > 0
+    assert int(out["score_sum"].sum()) >= 0
+    b.close()

@@ -7,7 +7,9 @@
 a) nn.Sequential fp32 (hipBLASLt GEMMs + tanh passes), b) both MLPs as one 66->1024 GEMM +
 batched (2, M, k) GEMMs per layer (fp32), c) a) under bf16 autocast, d) b) in bf16, e) the
 fused gfx950 kernel ms_policy_forward (f32-input MFMA, activations in registers; marlsoccer.policy),
-f) e) with the RunningMeanStd normalisation fused (raw rows in, float64 normalisation in-kernel).
+f) e) with the RunningMeanStd normalisation fused (raw rows in, float64 normalisation in-kernel),
+g) ms_policy_run as DeviceRollout launches it: the env's (N, 4, 66) obs rows of the blue agents,
+sampling, log-prob, obs storage copy and the env's action rows.
 Prints ms per forward and the max |difference| of the action mean and value against a).
 """
 from __future__ import annotations
@@ -76,6 +78,18 @@ def main():
         fp.forward(x, mean0, den1, act_mean=am, value=vv)
         return am, vv[:, None]
 
+    # the rollout step's launch (DeviceRollout): (N, 4, 66) env obs rows, sampling, every output
+    xo = torch.randn(a.envs, 4, 66, device=dev).clamp(-10, 10)
+    eps = torch.randn(M, 3, device=dev)
+    red = torch.rand(M, 3, device=dev)
+    act, lp, obs_copy = torch.empty((M, 3), device=dev), torch.empty((M,), device=dev), torch.empty((M, 66), device=dev)
+    env_act = torch.empty((a.envs, 4, 3), device=dev)
+
+    def kern_rollout():
+        fp.run(xo, M, 2, 264, 66, mean0, den1, eps=eps, act_mean=am, action=act, logprob=lp, value=vv,
+               obs_copy=obs_copy, env_actions=env_act, red_uniform=red)
+        return am, vv[:, None]
+
     variants = {
         "sequential_fp32": seq,
         "fused_fp32": lambda: fused(p32, torch.float32),
@@ -83,9 +97,12 @@ def main():
         "fused_bf16": lambda: fused(p16, torch.bfloat16),
         "ms_policy_forward": kern,
         "ms_policy_forward_normalising": kern_norm,
+        "ms_policy_run_rollout_io": kern_rollout,
     }
     with torch.no_grad():
         ref_mu, ref_v = seq()
+        xb = xo[:, :2].reshape(M, 66)
+        refs = {"ms_policy_run_rollout_io": (agent.actor_mean(xb), agent.critic(xb))}
         for name, fn in variants.items():
             for _ in range(3):
                 fn()
@@ -98,8 +115,9 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
             print(json.dumps({"variant": name, "rows": M, "ms_per_forward": ms, "tflops": 824192 * 2 * M / 2 / ms / 1e9,
-                              "max_abs_diff_mean": float((mu.float() - ref_mu).abs().max()),
-                              "max_abs_diff_value": float((v.float() - ref_v).abs().max())}), flush=True)
+                              "max_abs_diff_mean": float((mu.float() - refs.get(name, (ref_mu,))[0]).abs().max()),
+                              "max_abs_diff_value": float((v.float() - refs.get(name, (0, ref_v))[1]).abs().max())}),
+                  flush=True)
 
 
 if __name__ == "__main__":
