@@ -353,8 +353,11 @@ class FrameRingBatch(SoccerBatch):
     contiguous layout holds (soccer_env.py:130-140). The view is valid until the next step or
     reset moves the window; copy it (or index the ring with `window_index`) to keep it. Every
     R - 2 steps the window moves back to the ring's start and that step writes all three
-    frames. An env not stepped because of a non-finite action keeps stale frames in its window
-    (SoccerBatch leaves its previous observation; both raise via raise_if_nonfinite).
+    frames. An env not stepped because of a non-finite action writes no frame, and the window
+    still advances: its window holds a stale frame (zeros or one from R - 2 steps back) until two
+    more valid steps have pushed it out, whereas SoccerBatch's contiguous obs keeps the previous
+    observation. Both raise via raise_if_nonfinite; after catching that ValueError, call
+    reset(mask=...) for that env before reading its window again.
     """
 
     def __init__(self, num_envs: int, ring: int = 32, **kw):

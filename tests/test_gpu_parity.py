@@ -290,27 +290,37 @@ def test_actions_out_of_range_are_clipped(ms):
 
 # ---- full-size properties (BASELINE configs) ------------------------------------------------
 
-@pytest.mark.parametrize("n,max_steps,steps,env0", [(4096, 50, 120, 0), (8192, 1000, 120, 3 * 8192),
-                                                    (32768, 512, 560, 5 * 32768), (65536, 50, 120, 0)])
-def test_full_size_subsample_and_invariants(ms, n, max_steps, steps, env0):
-    """BASELINE config sizes: 4,096 and 65,536 envs per GPU (configs 1-2), rank 3's shard of
-    config 4 (65,536 envs / 8 GPUs = 8,192, global envs 24,576..32,767) and rank 5's shard of
-    config 5 (262,144 / 8 = 32,768, max_steps=512, default reward shaping, a whole episode plus
-    its auto-reset). A shard is seeded and driven by its global env indices (seed 19 + g, actions
-    a function of g), as bench.py and marlsoccer.distributed do. The 64-env subsample matches the
-    fp32 oracle bit for bit, state stays finite and inside the field, results are independent of
-    the batch they run in."""
+@pytest.mark.parametrize("n,max_steps,steps,env0", [
+    pytest.param(4096, 1000, 1020, 0, id="configs1-4096envs-whole-episode"),
+    pytest.param(65536, 1000, 1020, 0, id="configs2-65536envs-whole-episode"),
+    pytest.param(8192, 1000, 120, 3 * 8192, id="configs3-rank3-shard-8192envs-120steps"),
+    pytest.param(32768, 512, 560, 5 * 32768, id="configs4-rank5-shard-32768envs-maxsteps512-whole-episode"),
+])
+def test_config_sizes_hash_actions_subsample(ms, n, max_steps, steps, env0):
+    """The BASELINE configs' per-GPU batch sizes, with deterministic hash actions (a function of
+    the global env index and the step; configs 1-2 over a whole 1,000-step episode plus its
+    auto-reset, config 3's rank-3 shard (65,536 envs / 8 GPUs = 8,192, global envs
+    24,576..32,767) for 120 steps, config 4's rank-5 shard (262,144 / 8 = 32,768, max_steps=512)
+    over a whole episode plus its auto-reset). A shard is seeded and driven by its global env
+    indices (seed 19 + g), as bench.py and marlsoccer.distributed do. Every 20th step the obs of
+    a 64-env subsample match the fp32 oracle bit for bit; at the end state is finite and inside
+    the field, no arbiter overflowed. (Device-Philox uniform actions as in the bench:
+    test_config5_whole_batch_one_gpu_subsample.)"""
     gpu = ms.SoccerBatch(n, config=cfg_dict(max_steps=max_steps))
     gpu.reset(seed=19 + env0)
     sub = np.linspace(0, n - 1, 64).astype(np.int64)
+    sub_d = torch.from_numpy(sub).to(gpu.device)
     ref = orc.OracleBatch(64, "f32", oracle_cfg(gpu._cfg))
     ref.reset(np.stack([orc.pcg_from_seed(19 + env0 + int(i)) for i in sub]), 0)
+    dones = 0
     for t in range(steps):
         act = sh.hash_actions(n, t, env0=env0)
         out = gpu.step(torch.from_numpy(act).to(gpu.device))
-        robs = ref.step(act[sub])[0]
-        if t % 20 == 19:
-            np.testing.assert_array_equal(out.obs.cpu().numpy()[sub], robs, err_msg=f"t={t}")
+        robs, _, rtrunc = ref.step(act[sub])[:3]
+        dones += int(rtrunc[:, 0].sum())
+        if t % 20 == 19 or t == max_steps - 1:
+            np.testing.assert_array_equal(out.obs[sub_d].cpu().numpy(), robs, err_msg=f"t={t}")
+    assert dones == 64 * (steps // max_steps)
     st = gpu.export_state()
     assert np.isfinite(st["body"]["px"]).all() and np.isfinite(st["body"]["vx"]).all()
     assert (st["body"]["px"] > -50).all() and (st["body"]["px"] < 850).all()
