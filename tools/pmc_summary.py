@@ -84,7 +84,7 @@ def main(tag, envs=65536, kernel="ms_step_kernel", warmup=1000, steps=1000, max_
         # gfx950; the compiler's own resource usage is "compiler"
         "regimes": {},
     }
-    for w, s in ((5, 20), (1000, 200)):
+    for w, s in ((5, 20), (1000, 200), (1000, 1000)):
         r = window_pmc(src, kernel, envs, w, s)
         if r is not None:
             out["regimes"][f"e{envs}_ms{max_steps}_w{w}_s{s}"] = r
