@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--persistent", type=int, default=None, metavar="W",
                     help="ms_step launch shape (SoccerBatch.set_persistent): W waves persistent, 0 one wave per "
                          "block, -1 one wave per SIMD; default: the library's")
+    ap.add_argument("--lane-group", type=int, default=None, metavar="G",
+                    help="ms_step kernel (SoccerBatch.set_lane_group): G = 8 or 16 lanes per env, 0 one lane per "
+                         "env, -1 automatic; default: the library's (8 lanes while envs x 8 fit the SIMDs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ring-leg", action="store_true", help="skip the frame-ring leg timed beside the headline")
     ap.add_argument("--cpu-envs", type=int, default=65536)
@@ -196,6 +199,8 @@ def main():
              SoccerBatch(E, config=cfg, device=dev.index))
     if args.persistent is not None and not ring:
         batch.set_persistent(args.persistent)
+    if args.lane_group is not None and not ring:
+        batch.set_lane_group(args.lane_group)
     batch.reset(seed=19 + rank * E)  # env i of rank r seeded 19 + r*E + i (global index)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
@@ -372,7 +377,9 @@ def main():
                                     else ""),
                        "envs_per_gpu": E, "global_envs": world * E, "max_steps": args.max_steps,
                        "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else ""),
-                       "launch": (f"persistent, {batch.persistent_waves} waves" if not ring and
+                       "launch": (f"lane groups, {batch.lane_group} lanes per env ({64 // batch.lane_group} envs "
+                                  "per wave)" if not ring and batch.lane_group > 0 else
+                                  f"persistent, {batch.persistent_waves} waves" if not ring and
                                   batch.persistent_waves > 0 and (E + 63) // 64 > batch.persistent_waves
                                   else "one wave per 64-env block"),
                        **({"obs_layout": f"frame ring, R = {ring} (opt-in; obs is a strided (N, 4, 66) window)"}

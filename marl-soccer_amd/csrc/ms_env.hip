@@ -735,8 +735,21 @@ __device__ __forceinline__ float body_iinv(const Params& P, int b) {
 __device__ __forceinline__ float body_b_minv(const Params& P, int b) { return b < 4 ? P.m_inv[0] : 0.0f; }
 __device__ __forceinline__ float body_b_iinv(const Params& P, int b) { return b < 4 ? P.i_inv[0] : 0.0f; }
 
+// Body velocity records of the contact solve: the step kernel's per-lane LDS layout (LaneBodies)
+// or one env's records of the lane-group kernel (ms_group.inc). The contact arithmetic below is
+// shared, so both kernels compute every impulse with the same operations in the same order.
+struct LaneBodies {
+  Lds& L;
+  int lane;
+  __device__ __forceinline__ void ld_v(int b, V2& v, float& w) const { ::ld_v(L, b, lane, v, w); }
+  __device__ __forceinline__ void st_v(int b, V2 v, float w) const { ::st_v(L, b, lane, v, w); }
+  __device__ __forceinline__ void ld_vb(int b, V2& v, float& w) const { ::ld_vb(L, b, lane, v, w); }
+  __device__ __forceinline__ void st_vb(int b, V2 v, float w) const { ::st_vb(L, b, lane, v, w); }
+};
+
 // cpArbiterPreStep for one contact (velocities: previous step's post-solve values)
-__device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds& L, int lane) {
+template <class BR>
+__device__ __forceinline__ void prestep_t(const Params& P, CSlot& c, const BR& B) {
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
   const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_b_minv(P, bb), ib = body_b_iinv(P, bb);
   const int p = CS_PAIR(c.m);
@@ -747,8 +760,8 @@ __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds
   const V2 n = c.n;
   V2 va, vb;
   float wa, wbv;
-  ld_v(L, ba, lane, va, wa);
-  ld_v(L, bb, lane, vb, wbv);
+  B.ld_v(ba, va, wa);
+  B.ld_v(bb, vb, wbv);
   const V2 r1 = c.r1, r2 = c.r2;
   const float rcn1 = vcross(r1, n), rcn2 = vcross(r2, n);
   c.nMass = 1.0f / ((ma + ia * rcn1 * rcn1) + (mb + ib * rcn2 * rcn2));
@@ -762,9 +775,13 @@ __device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds
   const V2 v2s = vadd(vb, vmult(vperp(r2), wbv));
   c.bounce = vdot(vsub(v2s, v1), n) * e;
 }
+__device__ __forceinline__ void prestep_one(const Params& P, CSlot& c, const Lds& L, int lane) {
+  prestep_t(P, c, LaneBodies{const_cast<Lds&>(L), lane});
+}
 
 // cpArbiterApplyCachedImpulse for one contact (dt_coef = 1)
-__device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L, int lane) {
+template <class BR>
+__device__ __forceinline__ void warm_t(const Params& P, const CSlot& c, const BR& B) {
   if (!CS_WARM(c.m)) return;
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
   const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_b_minv(P, bb), ib = body_b_iinv(P, bb);
@@ -772,24 +789,27 @@ __device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L
   const V2 nj = vneg(j);
   V2 va, vb;
   float wa, wbv;
-  ld_v(L, ba, lane, va, wa);
-  st_v(L, ba, lane, vmadd(nj, ma, va), __builtin_fmaf(ia, vcross(c.r1, nj), wa));
-  ld_v(L, bb, lane, vb, wbv);
-  st_v(L, bb, lane, vmadd(j, mb, vb), __builtin_fmaf(ib, vcross(c.r2, j), wbv));
+  B.ld_v(ba, va, wa);
+  B.st_v(ba, vmadd(nj, ma, va), __builtin_fmaf(ia, vcross(c.r1, nj), wa));
+  B.ld_v(bb, vb, wbv);
+  B.st_v(bb, vmadd(j, mb, vb), __builtin_fmaf(ib, vcross(c.r2, j), wbv));
+}
+__device__ __forceinline__ void warm_one(const Params& P, const CSlot& c, Lds& L, int lane) {
+  warm_t(P, c, LaneBodies{L, lane});
 }
 
-// cpArbiterApplyImpulse for one contact
-__device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int lane) {
+// cpArbiterApplyImpulse for one contact, with its bodies' inverse masses and moments given
+template <class BR>
+__device__ __forceinline__ void solve_m(CSlot& c, const BR& B, float ma, float ia, float mb, float ib) {
   const int ba = CS_BA(c.m), bb = CS_BB(c.m);
-  const float ma = body_minv(P, ba), ia = body_iinv(P, ba), mb = body_b_minv(P, bb), ib = body_b_iinv(P, bb);
   const V2 n = c.n;
   const V2 r1 = c.r1, r2 = c.r2;
   V2 vba, vbb, va, vb;
   float wba, wbb, wa, wb_;
-  ld_vb(L, ba, lane, vba, wba);
-  ld_vb(L, bb, lane, vbb, wbb);
-  ld_v(L, ba, lane, va, wa);
-  ld_v(L, bb, lane, vb, wb_);
+  B.ld_vb(ba, vba, wba);
+  B.ld_vb(bb, vbb, wbb);
+  B.ld_v(ba, va, wa);
+  B.ld_v(bb, vb, wb_);
   const V2 vb1 = vmadd(vperp(r1), wba, vba);
   const V2 vb2 = vmadd(vperp(r2), wbb, vbb);
   const V2 vs1 = vmadd(vperp(r1), wa, va);
@@ -818,10 +838,18 @@ __device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int
   const V2 nj = vneg(j);
   // body a first, then body b (apply_bias_impulses then apply_impulses, cpArbiter.c);
   // a and b are distinct bodies, so the four updates commute per body.
-  st_vb(L, ba, lane, vmadd(njb, ma, vba), __builtin_fmaf(ia, vcross(r1, njb), wba));
-  st_vb(L, bb, lane, vmadd(jbv, mb, vbb), __builtin_fmaf(ib, vcross(r2, jbv), wbb));
-  st_v(L, ba, lane, vmadd(nj, ma, va), __builtin_fmaf(ia, vcross(r1, nj), wa));
-  st_v(L, bb, lane, vmadd(j, mb, vb), __builtin_fmaf(ib, vcross(r2, j), wb_));
+  B.st_vb(ba, vmadd(njb, ma, vba), __builtin_fmaf(ia, vcross(r1, njb), wba));
+  B.st_vb(bb, vmadd(jbv, mb, vbb), __builtin_fmaf(ib, vcross(r2, jbv), wbb));
+  B.st_v(ba, vmadd(nj, ma, va), __builtin_fmaf(ia, vcross(r1, nj), wa));
+  B.st_v(bb, vmadd(j, mb, vb), __builtin_fmaf(ib, vcross(r2, j), wb_));
+}
+template <class BR>
+__device__ __forceinline__ void solve_t(const Params& P, CSlot& c, const BR& B) {
+  const int ba = CS_BA(c.m), bb = CS_BB(c.m);
+  solve_m(c, B, body_minv(P, ba), body_iinv(P, ba), body_b_minv(P, bb), body_b_iinv(P, bb));
+}
+__device__ __forceinline__ void solve_one(const Params& P, CSlot& c, Lds& L, int lane) {
+  solve_t(P, c, LaneBodies{L, lane});
 }
 
 // Cross-lane hand-off through LDS inside one wave: every lane's LDS writes before it are
@@ -1787,6 +1815,9 @@ __global__ void ms_debug_rewards_kernel(Params P, int64_t n, const float* __rest
   rew[2 * e + 1] = r;
 }
 
+// small batches: one env per lane group (ms_step when envs x 8 <= the device's lanes)
+#include "ms_group.inc"
+
 // =============================================================================================
 // Host side: the C-ABI
 // =============================================================================================
@@ -1795,6 +1826,8 @@ struct ms_env {
   hipStream_t stream;
   int64_t n;
   int pipe_waves;  // ms_step: > 0 persistent grid of this many waves (0: one wave per block)
+  int group;       // ms_step: lanes per env of the lane-group kernel (8 or 16), 0: one lane per env
+  int64_t lanes;   // the device's wave slots at one wave per SIMD x 64 (4 x CUs x 64)
   Params P;
   bool default_params;  // P == default_params() up to max_steps/autoreset: specialised kernel
   DevState S;
@@ -1970,6 +2003,10 @@ int ms_config_specialised(const ms_config* cfg) {
 
 static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 
+// ms_step's default kernel: the lane-group kernel (8 lanes per env) while the batch fits the
+// device's SIMDs at one wave each with 8 lanes per env, the one-lane-per-env kernel above that
+static int auto_group(int64_t n, int64_t lanes) { return n * 8 <= lanes ? 8 : 0; }
+
 int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms_env** out) {
   if (!out || n_envs <= 0) return fail(MS_ERR_INVALID_ARGUMENT, "ms_create: n_envs must be > 0");
   if (n_envs > ((int64_t)1 << 31)) return fail(MS_ERR_INVALID_ARGUMENT, "ms_create: n_envs too large");
@@ -1988,6 +2025,8 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     h->pipe_waves = 4 * cus;
+    h->lanes = (int64_t)h->pipe_waves * 64;
+    h->group = auto_group(n_envs, h->lanes);
   }
   const size_t n = (size_t)n_envs;
   const size_t total = (size_t)((n + BLK - 1) / BLK) * BLOCK_BYTES;  // state blocks, the last one padded
@@ -2008,9 +2047,10 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
     return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of the contact spill buffer failed");
   }
 #ifdef MS_STAMPS
-  if (hipMalloc((void**)&h->S.stamps, sizeof(unsigned long long) * MS_NSTAMP * ((n + MS_BLOCK - 1) / MS_BLOCK)) != hipSuccess)
+  // one row per wave: 64-env blocks, or the lane-group kernel's waves of 64 / G envs (G <= 16)
+  if (hipMalloc((void**)&h->S.stamps, sizeof(unsigned long long) * MS_NSTAMP * ((n + 3) / 4)) != hipSuccess)
     return fail(MS_ERR_OUT_OF_MEMORY, "stamps");
-  (void)hipMemsetAsync(h->S.stamps, 0, sizeof(unsigned long long) * MS_NSTAMP * ((n + MS_BLOCK - 1) / MS_BLOCK), h->stream);
+  (void)hipMemsetAsync(h->S.stamps, 0, sizeof(unsigned long long) * MS_NSTAMP * ((n + 3) / 4), h->stream);
 #endif
   const size_t nblk = (n + BLK - 1) / BLK;
   if (hipMalloc((void**)&h->ctr, sizeof(Counters)) != hipSuccess ||
@@ -2086,7 +2126,25 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
       ((uintptr_t)trunc & 3u) || ((uintptr_t)score & 7u))
     return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: misaligned buffer (actions/rew 16 B, obs/score 8 B, flags 4 B)");
   const unsigned nblk = grid_for(h->n, MS_BLOCK);
-  if (h->pipe_waves > 0 && nblk > (unsigned)h->pipe_waves) {
+  if (h->group > 0) {
+    const int G = h->group;
+    const dim3 grid(grid_for(h->n, 64 / G));
+    if (G == 8) {
+      if (h->default_params)
+        hipLaunchKernelGGL((ms_step_group_kernel<true, 8>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew,
+                           term, trunc, goal, score, h->ctr);
+      else
+        hipLaunchKernelGGL((ms_step_group_kernel<false, 8>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs,
+                           rew, term, trunc, goal, score, h->ctr);
+    } else {
+      if (h->default_params)
+        hipLaunchKernelGGL((ms_step_group_kernel<true, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs,
+                           rew, term, trunc, goal, score, h->ctr);
+      else
+        hipLaunchKernelGGL((ms_step_group_kernel<false, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs,
+                           rew, term, trunc, goal, score, h->ctr);
+    }
+  } else if (h->pipe_waves > 0 && nblk > (unsigned)h->pipe_waves) {
     const dim3 grid((unsigned)h->pipe_waves);
     if (h->default_params)
       hipLaunchKernelGGL(ms_step_pipe_kernel<true>, grid, dim3(MS_BLOCK), 0, h->stream, h->S, h->P, actions, obs, rew,
@@ -2117,6 +2175,17 @@ int ms_set_persistent(ms_env* h, int waves) {
 }
 
 int ms_get_persistent(const ms_env* h) { return h ? h->pipe_waves : -1; }
+
+int ms_set_lane_group(ms_env* h, int lanes) {
+  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_lane_group: null handle");
+  if (lanes < 0) lanes = auto_group(h->n, h->lanes);
+  if (lanes != 0 && lanes != 8 && lanes != 16)
+    return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_lane_group: lanes per env must be 0, 8, 16 or negative (automatic)");
+  h->group = lanes;
+  return MS_OK;
+}
+
+int ms_get_lane_group(const ms_env* h) { return h ? h->group : -1; }
 
 // Frame-ring arguments: frames 16-B aligned, R even and >= 4, window pos..pos+2 inside the row.
 static int ring_check(const char* fn, const float* frames, int R, int pos, int wrap) {
@@ -2218,7 +2287,7 @@ int ms_get_stats(ms_env* h, ms_stats* out) {
 #ifdef MS_STAMPS
 int ms_debug_stamps(ms_env* h, void** ptr, int64_t* n_waves) {
   *ptr = h->S.stamps;
-  *n_waves = (h->n + MS_BLOCK - 1) / MS_BLOCK;
+  *n_waves = h->group > 0 ? (h->n + 64 / h->group - 1) / (64 / h->group) : (h->n + MS_BLOCK - 1) / MS_BLOCK;
   return MS_OK;
 }
 #endif

@@ -335,6 +335,17 @@ class SoccerBatch:
     def persistent_waves(self) -> int:
         return int(self._L.ms_get_persistent(self._h))
 
+    def set_lane_group(self, lanes: int = -1) -> None:
+        """ms_step's kernel (ms_set_lane_group): lanes = 8 or 16 steps each env with a group of
+        that many lanes (small batches: loads, per-body work, pair tests, prestep and frames
+        spread over the group); 0: one lane per env; -1: automatic (8 while envs x 8 fit the
+        device's SIMDs at one wave each, else 0). Results are identical either way."""
+        N.check(self._L.ms_set_lane_group(self._h, int(lanes)), "ms_set_lane_group")
+
+    @property
+    def lane_group(self) -> int:
+        return int(self._L.ms_get_lane_group(self._h))
+
     def synchronize(self) -> None:
         self.stream.synchronize()
 

@@ -362,14 +362,18 @@ def test_config5_whole_batch_one_gpu_subsample(ms):
     gpu.close()
 
 
-def test_corner_pileups_spill_path_bitexact(ms):
+@pytest.mark.parametrize("lanes", [0, 8, 16])
+def test_corner_pileups_spill_path_bitexact(ms, lanes):
     """All four agents and the ball wedged into the corners and pushed into them: more contacts
     per env than the kernel's 8 register slots: contacts 9-11 are staged in LDS for the solver and
     12+ stay in the global spill buffer (SP) — the rare paths of real play, held here for 80 steps
-    (up to 20 contacts per env) — bit for bit against the oracle."""
+    (up to 20 contacts per env) — bit for bit against the oracle. lanes 8/16: the lane-group
+    kernel (contacts in LDS, the solve's first 8 in registers, pair tests over the group)."""
     n = 64
     gpu = ms.SoccerBatch(n)  # default physics: the specialised kernel
     assert gpu.specialised
+    gpu.set_lane_group(lanes)
+    assert gpu.lane_group == lanes
     gpu.reset(seed=5)
     st = gpu.export_state()
     rng = np.random.default_rng(0)
@@ -447,7 +451,8 @@ def test_long_horizon_subsample_bitexact(ms):
     gpu.close()
 
 
-def test_obs_fallback_for_operands_outside_fast_domain_bitexact(ms):
+@pytest.mark.parametrize("lanes", [0, 8])
+def test_obs_fallback_for_operands_outside_fast_domain_bitexact(ms, lanes):
     """Frames whose operands fall outside the reduced-range division's domain (velocities and
     spins below 2^-100, in the t-2 snapshot, the step-start state and the new state) take the
     IEEE path for those lanes only; lanes of the same waves inside the domain keep the fast
@@ -455,6 +460,7 @@ def test_obs_fallback_for_operands_outside_fast_domain_bitexact(ms):
     n = 128
     gpu = ms.SoccerBatch(n)
     assert gpu.specialised
+    gpu.set_lane_group(lanes)
     gpu.reset(seed=11)
     for _ in range(3):  # leave the refilled stacks: the next steps emit t-2, t-1, t
         gpu.step(torch.zeros((n, 4, 3), device=gpu.device))
@@ -524,5 +530,62 @@ def test_persistent_launch_bitexact(ms, n, waves):
     assert sb["cache_entries_read"] == sa["cache_entries_read"]
     assert sb["cache_entries_written"] == sa["cache_entries_written"]
     assert sb["arbiter_overflow"] == 0
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("n,lanes,over", [
+    pytest.param(1000, 8, {}, id="1000envs-8lanes"),
+    pytest.param(333, 16, {}, id="333envs-16lanes"),
+    pytest.param(96, 8, dict(max_velocity=150, agent_mass=12, ball_mass=2, agent_friction=0.95,
+                             action_torque_max=800.0, goal_conceded_penalty=1.0), id="96envs-8lanes-generic"),
+])
+def test_lane_group_kernel_bitexact(ms, n, lanes, over):
+    """ms_step's lane-group kernel (ms_set_lane_group: G lanes per env, the default for batches
+    of at most the device's lanes / 8 envs) against the one-lane-per-env kernel and the fp32
+    oracle on every env: chase actions (goals, soft resets), episode ends and auto-resets
+    (max_steps 60), ragged last waves (1,000 and 333 envs). Obs, rewards, goals, scores and flags
+    at every step; the whole state (bodies, history, arbiter cache, RNG) and the cache tallies at
+    the end. The generic-parameter case runs the kernel instantiation without constant folding."""
+    steps = 150
+    cfg = cfg_dict(max_steps=60, **over)
+    a = ms.SoccerBatch(n, config=cfg)
+    b = ms.SoccerBatch(n, config=cfg)
+    a.set_lane_group(0)
+    b.set_lane_group(lanes)
+    assert a.lane_group == 0 and b.lane_group == lanes
+    assert a.specialised == (not over)
+    ref = orc.OracleBatch(n, "f32", oracle_cfg(a._cfg))
+    pcg = np.stack([orc.pcg_from_seed(29 + i) for i in range(n)])
+    a.reset(seed=29)
+    b.reset(seed=29)
+    ref.reset(pcg, 0)
+    rng = np.random.default_rng(29)
+    chaser = np.arange(n) % 4
+    goals = 0
+    for t in range(steps):
+        st = ref.export_state()
+        pos = np.stack([st["body"]["px"], st["body"]["py"]], -1)
+        act = sh.chase_actions(pos, st["body"]["angle"][:, :4], rng, chaser)
+        at = torch.from_numpy(act).to(a.device)
+        oa = a.step(at)
+        ob = b.step(at)
+        obs, rew, trunc, goal, score, bad = ref.step(act)
+        assert bad == 0
+        goals += int((goal != 0).sum())
+        np.testing.assert_array_equal(ob.obs.cpu().numpy(), obs, err_msg=f"obs t={t}")
+        np.testing.assert_array_equal(ob.rew.cpu().numpy(), rew.astype(np.float32), err_msg=f"rew t={t}")
+        np.testing.assert_array_equal(ob.goal.cpu().numpy(), goal, err_msg=f"goal t={t}")
+        np.testing.assert_array_equal(ob.score.cpu().numpy(), score, err_msg=f"score t={t}")
+        np.testing.assert_array_equal(ob.trunc.cpu().numpy().astype(bool), trunc, err_msg=f"trunc t={t}")
+        np.testing.assert_array_equal(oa.obs.cpu().numpy(), obs, err_msg=f"per-lane obs t={t}")
+    assert goals > 0 or n < 300, goals
+    assert_state_equal(b.export_state(), ref.export_state(), "lane-group end")
+    assert_state_equal(a.export_state(), ref.export_state(), "per-lane end")
+    sa, sb = a.stats(), b.stats()
+    assert sb["env_steps"] == sa["env_steps"] == n * steps
+    assert sb["cache_entries_read"] == sa["cache_entries_read"]
+    assert sb["cache_entries_written"] == sa["cache_entries_written"]
+    assert sb["arbiter_overflow"] == 0 and ref.overflow() == 0
     a.close()
     b.close()
