@@ -64,6 +64,15 @@ __device__ __forceinline__ float vlengthsq(V2 a) { return vdot(a, a); }
 __device__ __forceinline__ float fmaxr(float a, float b) { return (a > b) ? a : b; }  // cpfmax
 __device__ __forceinline__ float fminr(float a, float b) { return (a < b) ? a : b; }  // cpfmin
 __device__ __forceinline__ float fclamp(float f, float lo, float hi) { return fminr(fmaxr(f, lo), hi); }
+// fclamp(f, -M, M) (the friction clamp) by one v_med3_f32 instead of two compare-select pairs on
+// the solver's dependency chain: for M > 0 the median of (f, -M, M) is fclamp's value (bit for
+// bit for finite f: -M < f < M returns f itself, else the bound it crossed); for M <= 0 (or NaN)
+// fclamp returns M whatever f is (fmaxr(f, -M) >= -M >= M, then fminr(., M) = M, signed zeros
+// included)
+__device__ __forceinline__ float fclamp_sym(float f, float M) {
+  const float m = __builtin_amdgcn_fmed3f(f, -M, M);
+  return M > 0.0f ? m : M;
+}
 __device__ __forceinline__ float fclamp01(float f) { return fmaxr(0.0f, fminr(f, 1.0f)); }
 __device__ __forceinline__ V2 vlerp(V2 a, V2 b, float t) { return vadd(vmult(a, 1.0f - t), vmult(b, t)); }
 

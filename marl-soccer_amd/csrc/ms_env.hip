@@ -830,7 +830,7 @@ __device__ __forceinline__ void solve_m(CSlot& c, const BR& B, float ma, float i
   const float jtMax = c.u * c.jn;
   const float jt = -vrt * c.tMass;
   const float jtOld = c.jt;
-  c.jt = fclamp(jtOld + jt, -jtMax, jtMax);
+  c.jt = fclamp_sym(jtOld + jt, jtMax);
 
   const V2 jbv = vmult(n, c.jb - jbnOld);
   const V2 njb = vneg(jbv);
