@@ -240,6 +240,15 @@ int ms_get_persistent(const ms_env *env);
 int ms_set_lane_group(ms_env *env, int lanes);
 int ms_get_lane_group(const ms_env *env);
 
+/* The lane-group kernel's contact-solve schedule (Chipmunk's 10 Gauss-Seidel passes of
+ * cpSpaceStep, cpSpaceStep.c's solver loop, restated by oracle/soccer_oracle.c): mode 0
+ * (ms_create's default) picks per wave, 1 always solves each env's contacts in canonical order on
+ * two lanes (velocity and bias halves), 2 solves them in rounds by dependency level wherever the
+ * level schedule covers every env of the wave. Same results bit for bit in every mode; modes 1 and
+ * 2 exist so each path can be tested on its own. Host-only. */
+int ms_set_group_solve(ms_env *env, int mode);
+int ms_get_group_solve(const ms_env *env);
+
 /* Frame-ring observations (opt-in; replaces the deque of 3 frames of soccer_env.py:130-140
  * and marl_vecenv.py:30-68 with a window into a longer per-agent ring, so a step writes one
  * frame instead of three). `frames`: device float [N][4][R][22], 16-B aligned, R even >= 4.

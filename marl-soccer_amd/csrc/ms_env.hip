@@ -1827,6 +1827,7 @@ struct ms_env {
   int64_t n;
   int pipe_waves;  // ms_step: > 0 persistent grid of this many waves (0: one wave per block)
   int group;       // ms_step: lanes per env of the lane-group kernel (8 or 16), 0: one lane per env
+  int group_solve; // the lane-group kernel's contact-solve schedule (ms_set_group_solve)
   int64_t lanes;   // the device's wave slots at one wave per SIMD x 64 (4 x CUs x 64)
   Params P;
   bool default_params;  // P == default_params() up to max_steps/autoreset: specialised kernel
@@ -2132,17 +2133,17 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
     if (G == 8) {
       if (h->default_params)
         hipLaunchKernelGGL((ms_step_group_kernel<true, 8>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew,
-                           term, trunc, goal, score, h->ctr);
+                           term, trunc, goal, score, h->ctr, h->group_solve);
       else
         hipLaunchKernelGGL((ms_step_group_kernel<false, 8>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs,
-                           rew, term, trunc, goal, score, h->ctr);
+                           rew, term, trunc, goal, score, h->ctr, h->group_solve);
     } else {
       if (h->default_params)
         hipLaunchKernelGGL((ms_step_group_kernel<true, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs,
-                           rew, term, trunc, goal, score, h->ctr);
+                           rew, term, trunc, goal, score, h->ctr, h->group_solve);
       else
         hipLaunchKernelGGL((ms_step_group_kernel<false, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs,
-                           rew, term, trunc, goal, score, h->ctr);
+                           rew, term, trunc, goal, score, h->ctr, h->group_solve);
     }
   } else if (h->pipe_waves > 0 && nblk > (unsigned)h->pipe_waves) {
     const dim3 grid((unsigned)h->pipe_waves);
@@ -2186,6 +2187,16 @@ int ms_set_lane_group(ms_env* h, int lanes) {
 }
 
 int ms_get_lane_group(const ms_env* h) { return h ? h->group : -1; }
+
+int ms_set_group_solve(ms_env* h, int mode) {
+  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_group_solve: null handle");
+  if (mode < 0 || mode > 2)
+    return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_group_solve: mode must be 0 (automatic), 1 (serial) or 2 (rounds)");
+  h->group_solve = mode;
+  return MS_OK;
+}
+
+int ms_get_group_solve(const ms_env* h) { return h ? h->group_solve : -1; }
 
 // Frame-ring arguments: frames 16-B aligned, R even and >= 4, window pos..pos+2 inside the row.
 static int ring_check(const char* fn, const float* frames, int R, int pos, int wrap) {

@@ -346,6 +346,16 @@ class SoccerBatch:
     def lane_group(self) -> int:
         return int(self._L.ms_get_lane_group(self._h))
 
+    def set_group_solve(self, mode: int = 0) -> None:
+        """The lane-group kernel's contact-solve schedule (ms_set_group_solve): 0 automatic, 1
+        serial in canonical order, 2 rounds by dependency level. Results are identical in every
+        mode (the GPU parity tests run each)."""
+        N.check(self._L.ms_set_group_solve(self._h, int(mode)), "ms_set_group_solve")
+
+    @property
+    def group_solve(self) -> int:
+        return int(self._L.ms_get_group_solve(self._h))
+
     def synchronize(self) -> None:
         self.stream.synchronize()
 

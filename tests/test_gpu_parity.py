@@ -362,18 +362,22 @@ def test_config5_whole_batch_one_gpu_subsample(ms):
     gpu.close()
 
 
-@pytest.mark.parametrize("lanes", [0, 8, 16])
-def test_corner_pileups_spill_path_bitexact(ms, lanes):
+@pytest.mark.parametrize("lanes,solve", [(0, 0), (8, 0), (16, 0), (8, 2), (16, 2)],
+                         ids=["lanes0", "lanes8", "lanes16", "lanes8-rounds", "lanes16-rounds"])
+def test_corner_pileups_spill_path_bitexact(ms, lanes, solve):
     """All four agents and the ball wedged into the corners and pushed into them: more contacts
     per env than the kernel's 8 register slots: contacts 9-11 are staged in LDS for the solver and
     12+ stay in the global spill buffer (SP) — the rare paths of real play, held here for 80 steps
     (up to 20 contacts per env) — bit for bit against the oracle. lanes 8/16: the lane-group
-    kernel (contacts in LDS, the solve's first 8 in registers, pair tests over the group)."""
+    kernel (contacts in LDS, the solve's first 8 in registers, pair tests over the group);
+    solve 2: the contact solve in dependency-level rounds (two contacts per lane beyond 8 per env)
+    wherever a wave's envs have at most 16 contacts."""
     n = 64
     gpu = ms.SoccerBatch(n)  # default physics: the specialised kernel
     assert gpu.specialised
     gpu.set_lane_group(lanes)
-    assert gpu.lane_group == lanes
+    gpu.set_group_solve(solve)
+    assert gpu.lane_group == lanes and gpu.group_solve == solve
     gpu.reset(seed=5)
     st = gpu.export_state()
     rng = np.random.default_rng(0)
@@ -534,26 +538,34 @@ def test_persistent_launch_bitexact(ms, n, waves):
     b.close()
 
 
-@pytest.mark.parametrize("n,lanes,over", [
-    pytest.param(1000, 8, {}, id="1000envs-8lanes"),
-    pytest.param(333, 16, {}, id="333envs-16lanes"),
+@pytest.mark.parametrize("n,lanes,over,solve", [
+    pytest.param(1000, 8, {}, 0, id="1000envs-8lanes"),
+    pytest.param(1000, 8, {}, 1, id="1000envs-8lanes-serial"),
+    pytest.param(1000, 8, {}, 2, id="1000envs-8lanes-rounds"),
+    pytest.param(333, 16, {}, 0, id="333envs-16lanes"),
+    pytest.param(333, 16, {}, 2, id="333envs-16lanes-rounds"),
     pytest.param(96, 8, dict(max_velocity=150, agent_mass=12, ball_mass=2, agent_friction=0.95,
-                             action_torque_max=800.0, goal_conceded_penalty=1.0), id="96envs-8lanes-generic"),
+                             action_torque_max=800.0, goal_conceded_penalty=1.0), 0, id="96envs-8lanes-generic"),
+    pytest.param(96, 8, dict(max_velocity=150, agent_mass=12, ball_mass=2, agent_friction=0.95,
+                             action_torque_max=800.0, goal_conceded_penalty=1.0), 2, id="96envs-8lanes-generic-rounds"),
 ])
-def test_lane_group_kernel_bitexact(ms, n, lanes, over):
+def test_lane_group_kernel_bitexact(ms, n, lanes, over, solve):
     """ms_step's lane-group kernel (ms_set_lane_group: G lanes per env, the default for batches
     of at most the device's lanes / 8 envs) against the one-lane-per-env kernel and the fp32
     oracle on every env: chase actions (goals, soft resets), episode ends and auto-resets
     (max_steps 60), ragged last waves (1,000 and 333 envs). Obs, rewards, goals, scores and flags
     at every step; the whole state (bodies, history, arbiter cache, RNG) and the cache tallies at
-    the end. The generic-parameter case runs the kernel instantiation without constant folding."""
+    the end. The generic-parameter case runs the kernel instantiation without constant folding.
+    solve (ms_set_group_solve) runs the contact solve's automatic choice, the serial halves only
+    or the dependency-level rounds wherever they apply."""
     steps = 150
     cfg = cfg_dict(max_steps=60, **over)
     a = ms.SoccerBatch(n, config=cfg)
     b = ms.SoccerBatch(n, config=cfg)
     a.set_lane_group(0)
     b.set_lane_group(lanes)
-    assert a.lane_group == 0 and b.lane_group == lanes
+    b.set_group_solve(solve)
+    assert a.lane_group == 0 and b.lane_group == lanes and b.group_solve == solve
     assert a.specialised == (not over)
     ref = orc.OracleBatch(n, "f32", oracle_cfg(a._cfg))
     pcg = np.stack([orc.pcg_from_seed(29 + i) for i in range(n)])
