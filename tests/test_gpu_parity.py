@@ -57,9 +57,12 @@ def assert_state_equal(gpu_st, orc_st, where=""):
                                           err_msg=f"{where} env {i} arb.{f}")
 
 
-def run_pair(ms, n, steps, seed=19, mode_opts=None, chase=True, check_state_every=50, **over):
+def run_pair(ms, n, steps, seed=19, mode_opts=None, chase=True, check_state_every=50, lanes=None, **over):
     config = cfg_dict(**over)
     gpu = ms.SoccerBatch(n, config=config, autoreset=True)
+    if lanes is not None:  # 0: the per-lane kernel, 8: the lane-group kernel (the default below 8,192 envs)
+        gpu.set_lane_group(lanes)
+        assert gpu.lane_group == lanes
     ocfg = oracle_cfg(ms.to_ms_config(config, True))
     ref = orc.OracleBatch(n, "f32", ocfg)
     mode = ms.spawn_mode(mode_opts)
@@ -109,8 +112,9 @@ def test_reset_modes_bitexact(ms):
         gpu.close()
 
 
-def test_trajectory_chase_bitexact(ms):
-    c = run_pair(ms, 128, 1100, seed=19)
+@pytest.mark.parametrize("lanes", [0, 8], ids=["per-lane", "lane-group"])
+def test_trajectory_chase_bitexact(ms, lanes):
+    c = run_pair(ms, 128, 1100, seed=19, lanes=lanes)
     assert c["goals"] > 10 and c["dones"] == 128, c
 
 
@@ -118,13 +122,15 @@ def test_trajectory_random_bitexact(ms):
     run_pair(ms, 256, 400, seed=3, chase=False, check_state_every=100)
 
 
-def test_short_episodes_full_random_bitexact(ms):
+@pytest.mark.parametrize("lanes", [0, 8], ids=["per-lane", "lane-group"])
+def test_short_episodes_full_random_bitexact(ms, lanes):
     c = run_pair(ms, 96, 500, seed=5, mode_opts={"use_full_random_positions": True}, max_steps=70,
-                 score_difference_multiplier=5.0, goal_conceded_penalty=1.0)
+                 score_difference_multiplier=5.0, goal_conceded_penalty=1.0, lanes=lanes)
     assert c["dones"] >= 96 * 7 and c["goals"] > 0, c
 
 
-def test_nondefault_physics_generic_kernel_bitexact(ms):
+@pytest.mark.parametrize("lanes", [0, 8], ids=["per-lane", "lane-group"])
+def test_nondefault_physics_generic_kernel_bitexact(ms, lanes):
     """A config with other physics (speed cap, masses, damping, torque) runs the generic step
     kernel (parameters from the kernel arguments), bit for bit against the oracle."""
     over = dict(max_velocity=150, agent_mass=12, ball_mass=2, agent_friction=0.95, ball_friction=0.9,
@@ -132,7 +138,7 @@ def test_nondefault_physics_generic_kernel_bitexact(ms):
     from marlsoccer import _native as N
     from marlsoccer.config import to_ms_config
     assert not N.config_specialised(to_ms_config(cfg_dict(**over), True))
-    c = run_pair(ms, 96, 400, seed=23, **over)
+    c = run_pair(ms, 96, 400, seed=23, lanes=lanes, **over)
     assert c["dones"] >= 96 * 2, c
 
 
@@ -207,9 +213,11 @@ def test_gpu_terminal_override(ms):
 
 # ---- edge cases --------------------------------------------------------------------------
 
-def test_nonfinite_actions_skip_env_and_count(ms):
+@pytest.mark.parametrize("lanes", [0, 8], ids=["per-lane", "lane-group"])
+def test_nonfinite_actions_skip_env_and_count(ms, lanes):
     n = 64
     gpu = ms.SoccerBatch(n)
+    gpu.set_lane_group(lanes)
     gpu.reset(seed=1)
     before = gpu.export_state()
     act = torch.zeros((n, 4, 3), device=gpu.device)
@@ -270,13 +278,16 @@ def test_side_stream_ordering(ms):
 
 def test_single_env_and_ragged_sizes(ms):
     for n in (1, 63, 65, 1000):
-        c = run_pair(ms, n, 30, seed=n, chase=False, check_state_every=30)
-        assert c["dones"] == 0
+        for lanes in (0, 8):
+            c = run_pair(ms, n, 30, seed=n, chase=False, check_state_every=30, lanes=lanes)
+            assert c["dones"] == 0
 
 
-def test_actions_out_of_range_are_clipped(ms):
+@pytest.mark.parametrize("lanes", [0, 8], ids=["per-lane", "lane-group"])
+def test_actions_out_of_range_are_clipped(ms, lanes):
     n = 32
     gpu = ms.SoccerBatch(n)
+    gpu.set_lane_group(lanes)
     ref = orc.OracleBatch(n, "f32")
     gpu.reset(seed=2)
     ref.reset(np.stack([orc.pcg_from_seed(2 + i) for i in range(n)]), 0)
