@@ -149,14 +149,17 @@ def regime_key(envs: int, max_steps: int, warmup: int, steps: int) -> str:
     return f"e{envs}_ms{max_steps}_w{warmup}_s{steps}"
 
 
-def load_pmc_traffic(key: str):
+def load_pmc_traffic(key: str, kernel: str):
     """The committed rocprofv3 PMC figures of the step kernel over the same timed window
-    (dispatches warmup .. warmup + steps of a run with the same arguments), or None."""
+    (dispatches warmup .. warmup + steps of a run with the same arguments), or None — also when
+    the profiled launch ran another kernel than this run's (lane groups, persistent grid)."""
     path = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
     try:
         with open(path) as f:
             d = json.load(f)
         r = d["regimes"][key]
+        if r.get("kernel", d.get("kernel")) != kernel:
+            return None
         return dict(r, source=f"profiles/{d['tag']}_pmc.json", tag=d["tag"])
     except Exception:
         return None
@@ -216,6 +219,7 @@ def main():
 
     launch = (batch.launcher(actions, rew, term, trunc, goal, score) if ring else
               batch.launcher(actions, obs, rew, term, trunc, goal, score))
+    step_kernel = "ms_step_ring_kernel" if ring else batch.step_kernel  # the kernel the timed launches run
 
     nccl = world > 1 and dist.get_backend() == "nccl"
 
@@ -342,7 +346,7 @@ def main():
     value = world * E * args.steps / elapsed
     if rank == 0:
         key = regime_key(E, args.max_steps, args.warmup, args.steps)
-        pmc = None if ring else load_pmc_traffic(key)
+        pmc = None if ring else load_pmc_traffic(key, step_kernel)
         traffic = None
         pmc_info = None
         if pmc:
@@ -389,7 +393,7 @@ def main():
                          # the HBM bytes rocprofv3 measured (traffic) over the same time: the
                          # fraction of peak the launch really moves
                          "frac_measured": None if traffic is None else traffic / HBM_PEAK_GBS,
-                         "kernel": "ms_step_ring_kernel" if ring else "ms_step_kernel", "kernel_ms": kern_ms,
+                         "kernel": step_kernel, "kernel_ms": kern_ms,
                          "kernel_ms_method": "HIP events around the K back-to-back launches / K",
                          "alg_bytes_per_env_step": bytes_per_step,
                          "alg_bytes_source": ("SURVEY.md §8(d) without the prior frames' read and re-write: 881 + "
@@ -400,7 +404,7 @@ def main():
                          "traffic_source": (pmc_info["source"] + f" window {key} (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE "
                                             "per launch, same dispatches of a run with these arguments) over this "
                                             "run's kernel_ms") if traffic is not None else
-                                           f"no committed PMC pass for window {key}",
+                                           f"no committed PMC pass of {step_kernel} for window {key}",
                          # counted by the kernel over the timed launches (ms_stats tally)
                          "mean_cached_arbiters": mean_arb,
                          "cache_entries_per_env_step": {"read": arb_read, "written": arb_written,

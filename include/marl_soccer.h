@@ -175,7 +175,8 @@ typedef struct ms_stats {
   int64_t first_nonfinite_env;/* lowest env index with a non-finite action, -1 if none */
   /* Since the last ms_reset_stats, counted inside ms_step / ms_step_ring (ABI 2): env-steps
    * taken, and the arbiter-cache entries they read (the previous step's cache) and wrote (this
-   * step's), i.e. the warm-start cache traffic of the algorithmic byte count (20 B per entry). */
+   * step's), i.e. the warm-start cache traffic of the algorithmic byte count (20 B per entry).
+   * Kept as 64-bit counts per 64-env block on the device: they do not wrap within a run. */
   uint64_t env_steps;
   uint64_t cache_entries_read;
   uint64_t cache_entries_written;
@@ -248,6 +249,12 @@ int ms_get_lane_group(const ms_env *env);
  * 2 exist so each path can be tested on its own. Host-only. */
 int ms_set_group_solve(ms_env *env, int mode);
 int ms_get_group_solve(const ms_env *env);
+
+/* Name of the kernel the next ms_step launches for this handle's batch size and launch shape
+ * ("ms_step_kernel", "ms_step_pipe_kernel", "ms_step_group_kernel", ...), as rocprofv3 lists it
+ * (without template arguments): what bench.py's roofline line and its PMC lookup are keyed on.
+ * Host-only; "" for a null handle. */
+const char *ms_step_kernel_name(const ms_env *env);
 
 /* Frame-ring observations (opt-in; replaces the deque of 3 frames of soccer_env.py:130-140
  * and marl_vecenv.py:30-68 with a window into a longer per-agent ring, so a step writes one

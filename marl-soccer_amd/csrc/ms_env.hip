@@ -66,11 +66,17 @@ constexpr int OFF_CH = OFF_R2 + 2 * BLK * 16;
 constexpr int OFF_CJ = OFF_CH + 2 * MAXA * BLK * 4;
 constexpr int BLOCK_BYTES = OFF_CJ + 2 * MAXA * BLK * 16;
 
+// Per-block counts since ms_reset_stats, summed by ms_get_stats: arbiter-cache entries read (the
+// previous step's cache) and written, env-steps taken. 64-bit, so a block's counts never wrap.
+struct Tally {
+  unsigned long long read, written, steps, pad;
+};
+
 struct DevState {
   unsigned long long* stamps;  // MS_STAMPS diagnostic builds only: [wave][MS_NSTAMP] s_memtime
   char* blocks;                // [ceil(n / 64)] state blocks
   void* SP;  // contact slots KREG.. of each env (pile-ups only): [env][MAXC - KREG] CSlot
-  uint4* tally;  // [ceil(n / 64)] per-block counts since ms_reset_stats: cache entries read, written, env-steps
+  struct Tally* tally;  // [ceil(n / 64)] per-block counts since ms_reset_stats (64-bit: no wrap in a run)
   int64_t n;
 };
 
@@ -131,31 +137,6 @@ struct Counters {
 #define ACC_STORE(v, k) do { } while (0)
 #endif
 #define MS_NSTAMP 24
-
-// Diagnostic builds only (tools/maxilp_bisect.sh): a scheduling barrier at a phase boundary
-// when MS_SB_<phase> is defined, to find which region's instruction schedule changes results
-// under LLVM's max-ILP AMDGPU scheduler ("Faults"). Empty in the product build.
-#define MS_SB_IF(on) do { if (on) __builtin_amdgcn_sched_barrier(0); } while (0)
-#ifdef MS_SB_SOLVER
-#define MS_SB_SOLVER_ON 1
-#else
-#define MS_SB_SOLVER_ON 0
-#endif
-#ifdef MS_SB_NARROW
-#define MS_SB_NARROW_ON 1
-#else
-#define MS_SB_NARROW_ON 0
-#endif
-#ifdef MS_SB_PRESTEP
-#define MS_SB_PRESTEP_ON 1
-#else
-#define MS_SB_PRESTEP_ON 0
-#endif
-#ifdef MS_SB_OBS
-#define MS_SB_OBS_ON 1
-#else
-#define MS_SB_OBS_ON 0
-#endif
 
 // ---- per-lane env register file ------------------------------------------------------------
 struct Env {
@@ -1077,7 +1058,6 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
 #endif
   // narrowphase, one compacted loop per pair class so each lane visits only its own touching
   // pairs; class order + ctz order = canonical pair order (DESIGN.md pair table)
-  MS_SB_IF(MS_SB_NARROW_ON);
   while (mAA) {
     const int p = __builtin_ctz(mAA);
     mAA &= mAA - 1;
@@ -1196,7 +1176,6 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     if (col.count) add_arbiter(a, L, C, ovf, W, 42 + s, 4, 5, col, v2(0.0f, 0.0f), v2(0.0f, 0.0f), overflow_acc);
   }
   while (W.cur < W.nc_old) cache_age_current(a, L, W, overflow_acc);
-  MS_SB_IF(MS_SB_NARROW_ON);
   // contacts KREG.. of a pile-up from the global spill into LDS for the 12 passes over them
   // (the narrowphase scratch they share LDS with is dead from here on)
   asm volatile("" ::: "memory");
@@ -1222,7 +1201,6 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
     if (__ballot(PRE_GROUP * g < C.nc) != 0) {
       static_for<0, PRE_GROUP>([&](auto kc) __attribute__((always_inline)) {
         prestep_one(P, C.reg[PRE_GROUP * g + decltype(kc)::value], L, lane);
-        MS_SB_IF(MS_SB_PRESTEP_ON);
       });
     }
   });
@@ -1263,13 +1241,12 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
   if (need_h2) snap_load(a, h2);  // arrives during the solver
   if (C.nc > 0) {
     // cpArbiterApplyCachedImpulse, then cpArbiterApplyImpulse x 10 (pymunk Space default)
-    MS_SB_IF(MS_SB_SOLVER_ON);
-    FOR_CONTACTS(C, ovf, { warm_one(P, c_, L, lane); MS_SB_IF(MS_SB_SOLVER_ON); });
+    FOR_CONTACTS(C, ovf, { warm_one(P, c_, L, lane); });
     STAMP(15);
 #pragma unroll 1
     for (int it = 0; it < 10; ++it) {
       asm volatile("; MS_SOLVER_ITER_BEGIN" ::: "memory");
-      FOR_CONTACTS(C, ovf, { solve_one(P, c_, L, lane); MS_SB_IF(MS_SB_SOLVER_ON); });
+      FOR_CONTACTS(C, ovf, { solve_one(P, c_, L, lane); });
       asm volatile("; MS_SOLVER_ITER_END" ::: "memory");
     }
     STAMP(5);
@@ -1554,7 +1531,6 @@ __device__ __forceinline__ void step_block(const DevState& S, const Params& P, L
       emit_fill3(at, P, e, s0, obs);
       E.meta &= ~META_HE;
     } else {
-      MS_SB_IF(MS_SB_OBS_ON);
       if (obs) emit_three(P, h2, h1, s0, obs + e * 264);
       snap_store(at, h1);  // t-1 becomes the next step's t-2
     }
@@ -1574,10 +1550,10 @@ __device__ __forceinline__ void step_block(const DevState& S, const Params& P, L
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if (lane == 0) {
-      uint4* t = S.tally + blk;
-      atomicAdd(&t->x, v & 0xfffu);
-      atomicAdd(&t->y, (v >> 12) & 0xfffu);
-      atomicAdd(&t->z, v >> 24);
+      Tally* t = S.tally + blk;
+      atomicAdd(&t->read, (unsigned long long)(v & 0xfffu));
+      atomicAdd(&t->written, (unsigned long long)((v >> 12) & 0xfffu));
+      atomicAdd(&t->steps, (unsigned long long)(v >> 24));
     }
   }
 }
@@ -2055,14 +2031,14 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
 #endif
   const size_t nblk = (n + BLK - 1) / BLK;
   if (hipMalloc((void**)&h->ctr, sizeof(Counters)) != hipSuccess ||
-      hipMalloc((void**)&h->S.tally, sizeof(uint4) * nblk) != hipSuccess) {
+      hipMalloc((void**)&h->S.tally, sizeof(Tally) * nblk) != hipSuccess) {
     (void)hipFree(h->mem);
     (void)hipFree(h->S.SP);
     (void)hipFree(h->ctr);
     delete h;
     return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of counters failed");
   }
-  HIPCHK(hipMemsetAsync(h->S.tally, 0, sizeof(uint4) * nblk, h->stream));
+  HIPCHK(hipMemsetAsync(h->S.tally, 0, sizeof(Tally) * nblk, h->stream));
   HIPCHK(hipMemsetAsync(h->mem, 0, total, h->stream));
   Counters c0 = {0, 0, (long long)INT64_MAX};
   HIPCHK(hipMemcpyAsync(h->ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, h->stream));
@@ -2198,6 +2174,13 @@ int ms_set_group_solve(ms_env* h, int mode) {
 
 int ms_get_group_solve(const ms_env* h) { return h ? h->group_solve : -1; }
 
+const char* ms_step_kernel_name(const ms_env* h) {
+  if (!h) return "";
+  if (h->group > 0) return "ms_step_group_kernel";
+  if (h->pipe_waves > 0 && grid_for(h->n, MS_BLOCK) > (unsigned)h->pipe_waves) return "ms_step_pipe_kernel";
+  return "ms_step_kernel";
+}
+
 // Frame-ring arguments: frames 16-B aligned, R even and >= 4, window pos..pos+2 inside the row.
 static int ring_check(const char* fn, const float* frames, int R, int pos, int wrap) {
   if (!frames || ((uintptr_t)frames & 15u) || R < 4 || (R & 1) || pos < 0 || pos + 3 > R || (wrap != 0 && wrap != 1)) {
@@ -2279,17 +2262,17 @@ int ms_get_stats(ms_env* h, ms_stats* out) {
   out->nonfinite_envs = c.nonfinite;
   out->first_nonfinite_env = c.first_bad == (long long)INT64_MAX ? -1 : c.first_bad;
   const size_t nblk = (size_t)((h->n + BLK - 1) / BLK);
-  uint4* t = (uint4*)malloc(sizeof(uint4) * nblk);
+  Tally* t = (Tally*)malloc(sizeof(Tally) * nblk);
   if (!t) return fail(MS_ERR_OUT_OF_MEMORY, "ms_get_stats: host buffer");
-  if (hipMemcpy(t, h->S.tally, sizeof(uint4) * nblk, hipMemcpyDeviceToHost) != hipSuccess) {
+  if (hipMemcpy(t, h->S.tally, sizeof(Tally) * nblk, hipMemcpyDeviceToHost) != hipSuccess) {
     free(t);
     return fail(MS_ERR_HIP, "ms_get_stats: reading the per-block tally failed");
   }
   out->env_steps = out->cache_entries_read = out->cache_entries_written = 0;
   for (size_t b = 0; b < nblk; ++b) {
-    out->cache_entries_read += t[b].x;
-    out->cache_entries_written += t[b].y;
-    out->env_steps += t[b].z;
+    out->cache_entries_read += t[b].read;
+    out->cache_entries_written += t[b].written;
+    out->env_steps += t[b].steps;
   }
   free(t);
   return MS_OK;
@@ -2307,7 +2290,7 @@ int ms_reset_stats(ms_env* h) {
   if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_reset_stats: null handle");
   Counters c0 = {0, 0, (long long)INT64_MAX};
   HIPCHK(hipMemcpyAsync(h->ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemsetAsync(h->S.tally, 0, sizeof(uint4) * (size_t)((h->n + BLK - 1) / BLK), h->stream));
+  HIPCHK(hipMemsetAsync(h->S.tally, 0, sizeof(Tally) * (size_t)((h->n + BLK - 1) / BLK), h->stream));
   // c0 lives on this stack frame: the copy must have read it before the call returns
   HIPCHK(hipStreamSynchronize(h->stream));
   return MS_OK;

@@ -72,7 +72,7 @@ EXPORTED = (
     "ms_seed_pcg64_range", "ms_reset", "ms_step", "ms_observe", "ms_export_state", "ms_import_state",
     "ms_debug_rewards", "ms_get_stats", "ms_reset_stats", "ms_last_error", "ms_abi_version",
     "ms_config_specialised", "ms_step_ring", "ms_reset_ring", "ms_set_persistent", "ms_get_persistent",
-    "ms_set_lane_group", "ms_get_lane_group", "ms_set_group_solve", "ms_get_group_solve",
+    "ms_set_lane_group", "ms_get_lane_group", "ms_set_group_solve", "ms_get_group_solve", "ms_step_kernel_name",
     "ms_policy_forward", "ms_policy_last_error", "ms_policy_run", "ms_rollout_record",
 )
 
@@ -135,6 +135,9 @@ def lib():
         L.ms_set_lane_group.restype = C.c_int
         L.ms_get_lane_group.argtypes = [P]
         L.ms_get_lane_group.restype = C.c_int
+    if hasattr(L, "ms_step_kernel_name"):
+        L.ms_step_kernel_name.argtypes = [P]
+        L.ms_step_kernel_name.restype = C.c_char_p
     if hasattr(L, "ms_set_group_solve"):
         L.ms_set_group_solve.argtypes = [P, C.c_int]
         L.ms_set_group_solve.restype = C.c_int

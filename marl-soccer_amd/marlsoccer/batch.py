@@ -356,6 +356,11 @@ class SoccerBatch:
     def group_solve(self) -> int:
         return int(self._L.ms_get_group_solve(self._h))
 
+    @property
+    def step_kernel(self) -> str:
+        """Name of the kernel the next step launches (ms_step_kernel_name), as rocprofv3 lists it."""
+        return self._L.ms_step_kernel_name(self._h).decode()
+
     def synchronize(self) -> None:
         self.stream.synchronize()
 

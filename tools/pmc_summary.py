@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a gpurun_out/<tag>/ profiling run into profiles/ (tracked).
 
-Reads rocprofv3 CSVs written by tools/gpu_bench_profile.sh:
+Reads rocprofv3 CSVs written by `tools/gpu.sh profile`:
   trace/run_kernel_stats.csv          -> profiles/<tag>_kernel_stats.csv (copied verbatim)
   pmc_fetch|pmc_write/run_counter_collection.csv -> profiles/<tag>_pmc.json
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch (TCC_EA0 request counters). Per
@@ -60,6 +60,7 @@ def window_pmc(src, kernel, envs, warmup, steps):
         out["sgpr"] = int(rows[0]["SGPR_Count"])
         out["scratch_bytes_per_lane"] = int(rows[0]["Scratch_Size"])
         out["lds_bytes_per_block"] = int(rows[0]["LDS_Block_Size"])
+        out["kernel"] = rows[0]["Kernel_Name"].split("<")[0].split("(")[0].replace("void ", "").strip()
     fetch_kib, write_kib = statistics.median(vals["FETCH_SIZE"]), statistics.median(vals["WRITE_SIZE"])
     rd, wr = 2.0 * fetch_kib * 1024, write_kib * 1024
     out.update({"FETCH_SIZE_KiB_median": fetch_kib, "WRITE_SIZE_KiB_median": write_kib,
@@ -103,4 +104,5 @@ def main(tag, envs=65536, kernel="ms_step_kernel", warmup=1000, steps=1000, max_
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 65536)  # bench.py's default window
+    # tag [envs [kernel]]: bench.py's default window of the named step kernel
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 65536, sys.argv[3] if len(sys.argv) > 3 else "ms_step_kernel")

@@ -2,7 +2,7 @@
 """Build and time compile-time variants of the step kernel (diagnostic, not product code).
 
     python tools/variants.py build NAME="-DFOO=1 -DBAR=2" ...   # here: lib/variants/lib_NAME.so
-    python tools/variants.py build-ref REV NAME                  # ms_env.hip of git REV
+    python tools/variants.py build-ref REV NAME ["-DFOO=1 ..."]  # the step library of git REV
     python tools/variants.py run [--envs N] [--steps K] NAME ...  # on the GPU box
 
 `run` times each variant with bench.py (MARL_SOCCER_LIB points the loader at the variant) in
@@ -35,15 +35,19 @@ def main():
             name, _, defs = spec.partition("=")
             build(name, defs)
     elif a[0] == "build-ref":
-        rev, name = a[1], a[2]
-        src = os.path.join(PKG, "csrc", f"_ref_{name}.hip")
-        with open(src, "w") as f:
-            f.write(subprocess.run(["git", "-C", ROOT, "show", f"{rev}:marl-soccer_amd/csrc/ms_env.hip"],
-                                   check=True, capture_output=True, text=True).stdout)
+        # the whole source tree of REV (csrc/ and include/), so that ms_env.hip's includes
+        # (ms_device.h, ms_group.inc, marl_soccer.h) are that revision's, not the working tree's
+        import shutil
+        import tempfile
+        rev, name, defs = a[1], a[2], (a[3] if len(a) > 3 else "")
+        tmp = tempfile.mkdtemp(prefix="msref_")
         try:
-            build(name, "", src)
+            arc = subprocess.run(["git", "-C", ROOT, "archive", rev, "marl-soccer_amd/csrc", "include"],
+                                 check=True, capture_output=True).stdout
+            subprocess.run(["tar", "-x", "-C", tmp], input=arc, check=True)
+            build(name, defs, os.path.join(tmp, "marl-soccer_amd", "csrc", "ms_env.hip"))
         finally:
-            os.remove(src)
+            shutil.rmtree(tmp)
     elif a[0] == "run":
         envs, steps, names = "65536", "1000", []
         i = 1
