@@ -19,7 +19,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libmarlsoccer.so")
 SOURCES = [os.path.join(CSRC, "ms_env.hip"), os.path.join(CSRC, "ms_policy.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, "ms_device.h"), os.path.join(CSRC, "ms_group.inc"), os.path.join(ROOT, "include", "marl_soccer.h")]
+DEPS = SOURCES + [os.path.join(CSRC, "ms_device.h"), os.path.join(CSRC, "ms_group.inc"), os.path.join(CSRC, "ms_pair.inc"), os.path.join(ROOT, "include", "marl_soccer.h")]
 ARCH = os.environ.get("MS_OFFLOAD_ARCH", "gfx950")
 # LLVM's default AMDGPU machine scheduler. The max-ILP strategy (-mllvm
 # -amdgpu-sched-strategy=max-ilp, -2.6 % step time in round 1) produced kernels that fault on the

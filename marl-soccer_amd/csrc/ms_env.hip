@@ -75,7 +75,7 @@ struct Tally {
 struct DevState {
   unsigned long long* stamps;  // MS_STAMPS diagnostic builds only: [wave][MS_NSTAMP] s_memtime
   char* blocks;                // [ceil(n / 64)] state blocks
-  void* SP;  // contact slots KREG.. of each env (pile-ups only): [env][MAXC - KREG] CSlot
+  void* SP;  // contacts past an env's register / LDS slots (pile-ups only): [env][SPW] CSlot
   struct Tally* tally;  // [ceil(n / 64)] per-block counts since ms_reset_stats (64-bit: no wrap in a run)
   int64_t n;
 };
@@ -651,6 +651,9 @@ constexpr int KREG = 8;  // contacts held in registers; further ones go to the g
 constexpr int PRE_GROUP = 2;  // register slots per wave-uniform prestep group (2: 53.3 us, 4: 53.7, 8: 54.3, per-lane: 53.9)
 static_assert(KREG % PRE_GROUP == 0, "prestep groups must cover every register slot");
 #define MAXC (2 * MAXA)                 // contact capacity (2 per arbiter)
+// contact-spill slots per env (S.SP): the per-lane kernel spills contacts KREG.., the lane-pair
+// kernel contacts pr::KP.. (6), the lane-group kernel contacts grp::GCAP..
+constexpr int SPW = MAXC - 6;
 
 __device__ __forceinline__ void cache_write(At a, int par, int k, uint32_t hdr, float4 j) {
   *plane<uint32_t>(a, OFF_CH, par * MAXA + k) = hdr;
@@ -1039,7 +1042,7 @@ __device__ __forceinline__ void physics_step(const DevState& S, At a, int64_t e,
       if (bb_intersects(ballbb, P.seg[s].bb)) mBS |= 1u << s;
   }
 
-  CSlot* ovf = (CSlot*)S.SP + e * (MAXC - KREG);
+  CSlot* ovf = (CSlot*)S.SP + e * SPW;
   Contacts C;
   C.nc = 0;
   C.na = 0;
@@ -1793,6 +1796,8 @@ __global__ void ms_debug_rewards_kernel(Params P, int64_t n, const float* __rest
 
 // small batches: one env per lane group (ms_step when envs x 8 <= the device's lanes)
 #include "ms_group.inc"
+// two lanes per env, two waves per SIMD
+#include "ms_pair.inc"
 
 // =============================================================================================
 // Host side: the C-ABI
@@ -2018,7 +2023,7 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
   h->S.stamps = nullptr;
   // contact-slot spill for pile-ups beyond KREG contacts: reserved address space, touched
   // only by envs with more than KREG contacts (no traffic in ordinary play)
-  if (hipMalloc(&h->S.SP, sizeof(CSlot) * (MAXC - KREG) * n) != hipSuccess) {
+  if (hipMalloc(&h->S.SP, sizeof(CSlot) * SPW * n) != hipSuccess) {
     (void)hipFree(h->mem);
     delete h;
     return fail(MS_ERR_OUT_OF_MEMORY, "ms_create: hipMalloc of the contact spill buffer failed");
@@ -2103,7 +2108,15 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
       ((uintptr_t)trunc & 3u) || ((uintptr_t)score & 7u))
     return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: misaligned buffer (actions/rew 16 B, obs/score 8 B, flags 4 B)");
   const unsigned nblk = grid_for(h->n, MS_BLOCK);
-  if (h->group > 0) {
+  if (h->group == 2) {
+    const dim3 grid(grid_for(h->n, pr::EPW));
+    if (h->default_params)
+      hipLaunchKernelGGL(ms_step_pair_kernel<true>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew, term,
+                         trunc, goal, score, h->ctr);
+    else
+      hipLaunchKernelGGL(ms_step_pair_kernel<false>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew,
+                         term, trunc, goal, score, h->ctr);
+  } else if (h->group > 0) {
     const int G = h->group;
     const dim3 grid(grid_for(h->n, 64 / G));
     if (G == 8) {
@@ -2156,8 +2169,8 @@ int ms_get_persistent(const ms_env* h) { return h ? h->pipe_waves : -1; }
 int ms_set_lane_group(ms_env* h, int lanes) {
   if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_lane_group: null handle");
   if (lanes < 0) lanes = auto_group(h->n, h->lanes);
-  if (lanes != 0 && lanes != 8 && lanes != 16)
-    return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_lane_group: lanes per env must be 0, 8, 16 or negative (automatic)");
+  if (lanes != 0 && lanes != 2 && lanes != 8 && lanes != 16)
+    return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_lane_group: lanes per env must be 0, 2, 8, 16 or negative (automatic)");
   h->group = lanes;
   return MS_OK;
 }
@@ -2176,6 +2189,7 @@ int ms_get_group_solve(const ms_env* h) { return h ? h->group_solve : -1; }
 
 const char* ms_step_kernel_name(const ms_env* h) {
   if (!h) return "";
+  if (h->group == 2) return "ms_step_pair_kernel";
   if (h->group > 0) return "ms_step_group_kernel";
   if (h->pipe_waves > 0 && grid_for(h->n, MS_BLOCK) > (unsigned)h->pipe_waves) return "ms_step_pipe_kernel";
   return "ms_step_kernel";

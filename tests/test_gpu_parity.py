@@ -112,7 +112,11 @@ def test_reset_modes_bitexact(ms):
         gpu.close()
 
 
-@pytest.mark.parametrize("lanes", [0, 8], ids=["per-lane", "lane-group"])
+LANES = [0, 8, 2]
+LANE_IDS = ["per-lane", "lane-group", "lane-pair"]
+
+
+@pytest.mark.parametrize("lanes", LANES, ids=LANE_IDS)
 def test_trajectory_chase_bitexact(ms, lanes):
     c = run_pair(ms, 128, 1100, seed=19, lanes=lanes)
     assert c["goals"] > 10 and c["dones"] == 128, c
@@ -122,14 +126,14 @@ def test_trajectory_random_bitexact(ms):
     run_pair(ms, 256, 400, seed=3, chase=False, check_state_every=100)
 
 
-@pytest.mark.parametrize("lanes", [0, 8], ids=["per-lane", "lane-group"])
+@pytest.mark.parametrize("lanes", LANES, ids=LANE_IDS)
 def test_short_episodes_full_random_bitexact(ms, lanes):
     c = run_pair(ms, 96, 500, seed=5, mode_opts={"use_full_random_positions": True}, max_steps=70,
                  score_difference_multiplier=5.0, goal_conceded_penalty=1.0, lanes=lanes)
     assert c["dones"] >= 96 * 7 and c["goals"] > 0, c
 
 
-@pytest.mark.parametrize("lanes", [0, 8], ids=["per-lane", "lane-group"])
+@pytest.mark.parametrize("lanes", LANES, ids=LANE_IDS)
 def test_nondefault_physics_generic_kernel_bitexact(ms, lanes):
     """A config with other physics (speed cap, masses, damping, torque) runs the generic step
     kernel (parameters from the kernel arguments), bit for bit against the oracle."""
@@ -213,7 +217,7 @@ def test_gpu_terminal_override(ms):
 
 # ---- edge cases --------------------------------------------------------------------------
 
-@pytest.mark.parametrize("lanes", [0, 8], ids=["per-lane", "lane-group"])
+@pytest.mark.parametrize("lanes", LANES, ids=LANE_IDS)
 def test_nonfinite_actions_skip_env_and_count(ms, lanes):
     n = 64
     gpu = ms.SoccerBatch(n)
@@ -277,13 +281,13 @@ def test_side_stream_ordering(ms):
 
 
 def test_single_env_and_ragged_sizes(ms):
-    for n in (1, 63, 65, 1000):
-        for lanes in (0, 8):
+    for n in (1, 31, 33, 63, 65, 1000):
+        for lanes in LANES:
             c = run_pair(ms, n, 30, seed=n, chase=False, check_state_every=30, lanes=lanes)
             assert c["dones"] == 0
 
 
-@pytest.mark.parametrize("lanes", [0, 8], ids=["per-lane", "lane-group"])
+@pytest.mark.parametrize("lanes", LANES, ids=LANE_IDS)
 def test_actions_out_of_range_are_clipped(ms, lanes):
     n = 32
     gpu = ms.SoccerBatch(n)
@@ -373,8 +377,8 @@ def test_config5_whole_batch_one_gpu_subsample(ms):
     gpu.close()
 
 
-@pytest.mark.parametrize("lanes,solve", [(0, 0), (8, 0), (16, 0), (8, 2), (16, 2)],
-                         ids=["lanes0", "lanes8", "lanes16", "lanes8-rounds", "lanes16-rounds"])
+@pytest.mark.parametrize("lanes,solve", [(0, 0), (8, 0), (16, 0), (8, 2), (16, 2), (2, 0)],
+                         ids=["lanes0", "lanes8", "lanes16", "lanes8-rounds", "lanes16-rounds", "lanes2"])
 def test_corner_pileups_spill_path_bitexact(ms, lanes, solve):
     """All four agents and the ball wedged into the corners and pushed into them: more contacts
     per env than the kernel's 8 register slots: contacts 9-11 are staged in LDS for the solver and
@@ -466,7 +470,7 @@ def test_long_horizon_subsample_bitexact(ms):
     gpu.close()
 
 
-@pytest.mark.parametrize("lanes", [0, 8])
+@pytest.mark.parametrize("lanes", LANES, ids=LANE_IDS)
 def test_obs_fallback_for_operands_outside_fast_domain_bitexact(ms, lanes):
     """Frames whose operands fall outside the reduced-range division's domain (velocities and
     spins below 2^-100, in the t-2 snapshot, the step-start state and the new state) take the
@@ -559,6 +563,10 @@ def test_persistent_launch_bitexact(ms, n, waves):
                              action_torque_max=800.0, goal_conceded_penalty=1.0), 0, id="96envs-8lanes-generic"),
     pytest.param(96, 8, dict(max_velocity=150, agent_mass=12, ball_mass=2, agent_friction=0.95,
                              action_torque_max=800.0, goal_conceded_penalty=1.0), 2, id="96envs-8lanes-generic-rounds"),
+    pytest.param(1000, 2, {}, 0, id="1000envs-2lanes"),
+    pytest.param(333, 2, {}, 0, id="333envs-2lanes"),
+    pytest.param(96, 2, dict(max_velocity=150, agent_mass=12, ball_mass=2, agent_friction=0.95,
+                             action_torque_max=800.0, goal_conceded_penalty=1.0), 0, id="96envs-2lanes-generic"),
 ])
 def test_lane_group_kernel_bitexact(ms, n, lanes, over, solve):
     """ms_step's lane-group kernel (ms_set_lane_group: G lanes per env, the default for batches
@@ -610,5 +618,47 @@ def test_lane_group_kernel_bitexact(ms, n, lanes, over, solve):
     assert sb["cache_entries_read"] == sa["cache_entries_read"]
     assert sb["cache_entries_written"] == sa["cache_entries_written"]
     assert sb["arbiter_overflow"] == 0 and ref.overflow() == 0
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("n,max_steps,steps", [
+    pytest.param(32768, 512, 530, id="configs4-shard-32768envs-maxsteps512"),
+    pytest.param(65536, 1000, 150, id="configs2-65536envs"),
+])
+def test_lane_pair_full_size_equals_per_lane(ms, n, max_steps, steps):
+    """The lane-pair kernel (two lanes per env) against the one-lane-per-env kernel on every env of
+    a full-size batch (BASELINE configs[4]'s per-GPU shard across its auto-reset, configs[2]'s
+    65,536 envs): obs, rewards, flags, goals and scores compared on the device at every step, the
+    whole exported state at the end, and a 32-env subsample against the fp32 oracle."""
+    cfg = cfg_dict(max_steps=max_steps)
+    a = ms.SoccerBatch(n, config=cfg)
+    b = ms.SoccerBatch(n, config=cfg)
+    a.set_lane_group(0)
+    a.set_persistent(0)
+    b.set_lane_group(2)
+    assert b.step_kernel == "ms_step_pair_kernel" and a.step_kernel == "ms_step_kernel"
+    a.reset(seed=19)
+    b.reset(seed=19)
+    sub = np.linspace(0, n - 1, 32).astype(np.int64)
+    ref = orc.OracleBatch(len(sub), "f32", oracle_cfg(a._cfg))
+    ref.reset(np.stack([orc.pcg_from_seed(19 + int(i)) for i in sub]), 0)
+    gen = torch.Generator(device=a.device)
+    gen.manual_seed(77)
+    for t in range(steps):
+        act = torch.rand((n, 4, 3), generator=gen, device=a.device) * 2.0 - 1.0
+        oa = a.step(act)
+        ob = b.step(act)
+        for f in ("obs", "rew", "trunc", "goal", "score", "term"):
+            assert torch.equal(getattr(oa, f), getattr(ob, f)), f"{f} t={t}"
+        robs = ref.step(act[torch.from_numpy(sub).to(a.device)].cpu().numpy())[0]
+        if t % 25 == 24:
+            np.testing.assert_array_equal(ob.obs.cpu().numpy()[sub], robs, err_msg=f"oracle obs t={t}")
+    assert_state_equal(b.export_state(), a.export_state(), "end")
+    sa, sb = a.stats(), b.stats()
+    assert sb["env_steps"] == sa["env_steps"] == n * steps
+    assert sb["cache_entries_read"] == sa["cache_entries_read"]
+    assert sb["cache_entries_written"] == sa["cache_entries_written"]
+    assert sb["arbiter_overflow"] == 0
     a.close()
     b.close()

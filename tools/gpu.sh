@@ -30,7 +30,7 @@ suite() {
 parity() {
   local O=gpurun_out/$1; shift; mkdir -p $O
   local K=()
-  [ -n "$1" ] && K=(-k "$1")
+  [ -n "$1" ] && K=(-k "${1//+/ }")  # "+" stands for a space in the -k expression
   timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py "${K[@]}" > $O/pytest.log 2>&1 \
     || { tail -40 $O/pytest.log; return 1; }
   tail -1 $O/pytest.log
