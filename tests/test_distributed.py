@@ -197,3 +197,36 @@ def test_gloo_world2_sharded_equals_single_process():
     np.testing.assert_array_equal(got["goal"].numpy(), np.asarray(goal, np.int8))
     np.testing.assert_array_equal(got["score"].numpy(), np.asarray(score, np.int32))
     assert not got["term"].numpy().any()
+
+
+@pytest.mark.parametrize("shape,dtype", [((6, 4, 66), torch.float32), ((6, 1089), torch.uint8)],
+                         ids=["obs", "packed-outputs"])
+def test_all_gather_rows_rccl_branch_builds_the_gathered_tensor(monkeypatch, shape, dtype):
+    """all_gather_rows' RCCL branch (backend "nccl", distributed.py:72-75), which no CPU run
+    reaches: with torch.distributed's backend query and all_gather_into_tensor replaced by stand-ins,
+    the destination handed to the collective is (world x n, ...) of the input's dtype and device,
+    the input is passed unchanged, and the tensor returned is that destination (rank r's rows at
+    [r n, (r + 1) n))."""
+    from marlsoccer import distributed as D
+
+    world, calls = 4, []
+
+    def fake_all_gather_into_tensor(dst, src, group=None):
+        calls.append((tuple(dst.shape), dst.dtype, dst.device, src, group))
+        n = src.shape[0]
+        for r in range(world):  # what RCCL writes: rank r's buffer at rows [r n, (r + 1) n)
+            dst[r * n:(r + 1) * n] = src + r if dtype != torch.uint8 else src ^ r
+
+    monkeypatch.setattr(dist, "get_backend", lambda group=None: "nccl")
+    monkeypatch.setattr(dist, "all_gather_into_tensor", fake_all_gather_into_tensor)
+    src = (torch.arange(int(np.prod(shape))) % 251).reshape(shape).to(dtype)
+    group = object()
+    out = D.all_gather_rows(src, world, group)
+    assert len(calls) == 1
+    dshape, ddtype, ddev, csrc, cgroup = calls[0]
+    assert dshape == (world * shape[0],) + shape[1:] and ddtype == dtype and ddev == src.device
+    assert csrc is src and cgroup is group
+    assert out.shape == dshape and out.dtype == dtype
+    for r in range(world):
+        want = src + r if dtype != torch.uint8 else src ^ r
+        assert torch.equal(out[r * shape[0]:(r + 1) * shape[0]], want)
