@@ -157,6 +157,12 @@ class DeviceRollout:
     policy="fused" (the default for fp32): the normalisation and both MLPs run as ONE gfx950
     kernel (ms_policy_forward: f32-input MFMA, activations in registers; marlsoccer.policy),
     within 1e-5 of the torch modules; "torch": the modules themselves (hipBLASLt GEMMs).
+    Deviation of "fused": its tanh is the exp2/rcp form (~2e-7 absolute) and its log-prob uses
+    logstd directly instead of log(exp(logstd)), so the stored logprobs and values differ from the
+    torch Agent's by up to ~1e-5; a PPO update that recomputes log-probs with the torch modules
+    (the notebook's) starts its first epoch with exp(new - old) within 1e-4 of 1, not exactly 1
+    (tests/test_policy.py::test_fused_rollout_ppo_first_epoch_ratio_near_one). policy="torch"
+    keeps the notebook's bit-for-bit first-epoch ratio of 1.
     """
 
     def __init__(self, batch, agent: Agent, normalizer: RunningMeanStd, num_steps: int, seed: int = 0,

@@ -465,3 +465,36 @@ def test_fused_rollout_episode_bookkeeping():
     assert torch.isfinite(out["rewards"]).all() and float(out["rewards"].abs().sum()) > 0
     assert int(out["score_sum"].sum()) >= 0
     b.close()
+
+
+@pytest.mark.gpu
+def test_fused_rollout_ppo_first_epoch_ratio_near_one():
+    """The fused rollout's stored log-probs and values are the kernel's (tanh by exp2/rcp, log-prob
+    from logstd directly), not the torch modules': the PPO update recomputes them with
+    Agent.get_action_and_value on the stored obs and actions (notebook L340-380), so its first-epoch
+    ratio exp(new - old) is 1 only up to that difference. Over a 32-step rollout (goals, the
+    normaliser updating between steps as in training) the ratio stays within 1e-4 of 1 and the
+    values within 1e-4 (DeviceRollout's docstring states the deviation)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from marlsoccer import SoccerBatch
+    N, T = 1024, 32
+    torch.manual_seed(0)
+    agent = Agent().cuda()
+    with torch.no_grad():
+        agent.actor_logstd.copy_(torch.tensor([[-0.5, 0.0, 0.3]]))
+    rms = RunningMeanStd((66,), device="cuda")
+    rms.mean.copy_(torch.from_numpy(FX["run5_mean"]))
+    rms.var.copy_(torch.from_numpy(FX["run5_var"]))
+    b = SoccerBatch(N)
+    b.reset(seed=12)
+    ro = DeviceRollout(b, agent, rms, T, seed=3, update_normalizer=False)
+    assert ro.policy == "fused"
+    out = ro.collect()
+    with torch.no_grad():
+        x = rms.normalize(out["obs"].reshape(-1, 66))
+        _, newlogprob, _, newvalue = agent.get_action_and_value(x, out["actions"].reshape(-1, 3))
+    ratio = torch.exp(newlogprob - out["logprobs"].reshape(-1))
+    assert float((ratio - 1.0).abs().max()) <= 1e-4
+    assert float((newvalue.reshape(-1) - out["values"].reshape(-1)).abs().max()) <= 1e-4
+    b.close()
