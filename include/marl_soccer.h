@@ -232,12 +232,14 @@ int ms_step(ms_env *env, const float *actions, float *obs, float *rew, uint8_t *
 int ms_set_persistent(ms_env *env, int waves);
 int ms_get_persistent(const ms_env *env);
 
-/* ms_step's kernel for small batches. lanes = 8 or 16: a group of that many lanes steps each
- * env (a wave holds 64 / lanes envs), spreading loads, per-body work, the broadphase, the
- * narrowphase, prestep, cache writes and the observation frames over the group (replaces the
- * serial per-env loop of marl_vecenv.py:39 for batches that leave most SIMDs idle at one lane
- * per env); lanes = 0: one lane per env. Same results bit for bit. lanes < 0: automatic, which
- * is ms_create's default: 8 when n_envs x 8 <= the device's SIMDs x 64, else 0. Host-only. */
+/* ms_step's kernel by lanes per env (replaces the serial per-env loop of marl_vecenv.py:39).
+ * lanes = 8 or 16: a group of that many lanes steps each env (a wave holds 64 / lanes envs),
+ * spreading loads, per-body work, the broadphase, the narrowphase, prestep, cache writes and the
+ * observation frames over the group (small batches that leave most SIMDs idle at one lane per
+ * env). lanes = 2: a lane pair per env (32 envs per wave), each lane holding half of the env's
+ * working set, so the kernel fits 256 registers and two waves share each SIMD (batches that fill
+ * the SIMDs). lanes = 0: one lane per env. Same results bit for bit. lanes < 0: automatic, which
+ * is ms_create's default (ms_step_kernel_name names the kernel it picked). Host-only. */
 int ms_set_lane_group(ms_env *env, int lanes);
 int ms_get_lane_group(const ms_env *env);
 

@@ -338,8 +338,9 @@ class SoccerBatch:
     def set_lane_group(self, lanes: int = -1) -> None:
         """ms_step's kernel (ms_set_lane_group): lanes = 8 or 16 steps each env with a group of
         that many lanes (small batches: loads, per-body work, pair tests, prestep and frames
-        spread over the group); 0: one lane per env; -1: automatic (8 while envs x 8 fit the
-        device's SIMDs at one wave each, else 0). Results are identical either way."""
+        spread over the group); 2: a lane pair per env, two waves per SIMD (batches that fill
+        the device); 0: one lane per env; -1: automatic (the library's choice by batch size,
+        `step_kernel` names it). Results are identical either way."""
         N.check(self._L.ms_set_lane_group(self._h, int(lanes)), "ms_set_lane_group")
 
     @property
