@@ -652,8 +652,8 @@ constexpr int PRE_GROUP = 2;  // register slots per wave-uniform prestep group (
 static_assert(KREG % PRE_GROUP == 0, "prestep groups must cover every register slot");
 #define MAXC (2 * MAXA)                 // contact capacity (2 per arbiter)
 // contact-spill slots per env (S.SP): the per-lane kernel spills contacts KREG.., the lane-pair
-// kernel contacts pr::KP.. (6), the lane-group kernel contacts grp::GCAP..
-constexpr int SPW = MAXC - 6;
+// kernel contacts pr::KP.. (4-6), the lane-group kernel contacts grp::GCAP..
+constexpr int SPW = MAXC - 4;
 
 __device__ __forceinline__ void cache_write(At a, int par, int k, uint32_t hdr, float4 j) {
   *plane<uint32_t>(a, OFF_CH, par * MAXA + k) = hdr;

@@ -3,7 +3,7 @@
 
     python tools/variants.py build NAME="-DFOO=1 -DBAR=2" ...   # here: lib/variants/lib_NAME.so
     python tools/variants.py build-ref REV NAME ["-DFOO=1 ..."]  # the step library of git REV
-    python tools/variants.py run [--envs N] [--steps K] NAME ...  # on the GPU box
+    python tools/variants.py run [--envs N] [--steps K] [--lane-group G] [--max-steps M] NAME ...  # on the GPU box
 
 `run` times each variant with bench.py (MARL_SOCCER_LIB points the loader at the variant) in
 child processes, one after another, and prints one line per variant.
@@ -23,7 +23,8 @@ def build(name, defs, src=None):
     import build_native
     os.makedirs(VDIR, exist_ok=True)
     out = os.path.join(VDIR, f"lib_{name}.so")
-    cmd = [build_native.hipcc(), *build_native.FLAGS, *defs.split(), "-o", out, src or build_native.SOURCES[0]]
+    srcs = [src] + build_native.SOURCES[1:] if src else build_native.SOURCES
+    cmd = [build_native.hipcc(), *build_native.FLAGS, *defs.split(), "-o", out, *srcs]
     subprocess.run(cmd, check=True)
     print("built", out)
 
@@ -49,19 +50,21 @@ def main():
         finally:
             shutil.rmtree(tmp)
     elif a[0] == "run":
-        envs, steps, names = "65536", "1000", []
+        envs, steps, names, extra = "65536", "1000", [], []
         i = 1
         while i < len(a):
             if a[i] == "--envs":
                 envs = a[i + 1]; i += 2
             elif a[i] == "--steps":
                 steps = a[i + 1]; i += 2
+            elif a[i] in ("--lane-group", "--max-steps", "--warmup", "--persistent"):
+                extra += [a[i], a[i + 1]]; i += 2
             else:
                 names.append(a[i]); i += 1
         for name in names:
             env = dict(os.environ, MARL_SOCCER_LIB=os.path.join(VDIR, f"lib_{name}.so"))
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-ring-leg", "--envs", envs,
-                                "--steps", steps], env=env, capture_output=True, text=True, timeout=300)
+                                "--steps", steps, *extra], env=env, capture_output=True, text=True, timeout=300)
             if r.returncode != 0:
                 print(name, "FAILED", r.stderr[-2000:], flush=True)
                 sys.exit(1)
