@@ -9,7 +9,7 @@
 #                                               passes over the driver's and the default window
 #   tools/gpu.sh configs  <tag>                 the BASELINE configs' per-GPU batch sizes
 #   tools/gpu.sh sq       <tag> <envs> [bench args]  SQ counter passes (steady window: warm-up 1000, 100 steps)
-#   tools/gpu.sh stamps   <tag> <envs...>       per-phase wave stamps (tools/stamps.py; stamps library prebuilt)
+#   tools/gpu.sh stamps   <tag> [G=lanes] <envs...>  per-phase wave stamps (tools/stamps.py; stamps library prebuilt)
 #   tools/gpu.sh rehearse <tag>                 bench.py --gpus 2 with both ranks on cuda:0 (gloo), 2 x 8,192 and 2 x 65,536
 #   tools/gpu.sh policy   <tag>                 policy/rollout GPU tests + bench_policy + graph rollouts
 #
@@ -93,11 +93,13 @@ sq() {  # tag envs bench-args...
   rm -rf $O/p1 $O/p2 $O/p3  # the raw per-dispatch CSVs exceed gpurun's 64-MiB copy-back
 }
 
-stamps() {
+stamps() {  # tag [G=lanes] envs...
   local T=$1; shift
   local O=gpurun_out/$T; mkdir -p $O
+  local LG=()
+  case "$1" in G=*) LG=(--lane-group ${1#G=}); shift;; esac
   for N in "$@"; do
-    timeout -k 10 240 python tools/stamps.py --envs $N --steps 300 --warmup 1000 --every 10 --out $O/stamps_$N.json > $O/stamps_$N.log 2>&1 || { tail $O/stamps_$N.log; return 1; }
+    timeout -k 10 240 python tools/stamps.py --envs $N --steps 300 --warmup 1000 --every 10 "${LG[@]}" --out $O/stamps_$N.json > $O/stamps_$N.log 2>&1 || { tail $O/stamps_$N.log; return 1; }
     python -c "import json; d=json.load(open('$O/stamps_$N.json')); print($N, d['launch'], 'mean', round(d['wave_cycles_mean']), 'worst', round(d.get('worst_wave_cycles_mean', 0)), {k: round(v['mean']) for k, v in d['phases'].items()})"
   done
 }
