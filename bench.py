@@ -64,12 +64,10 @@ def parse():
     ap.add_argument("--frame-ring", type=int, default=0, metavar="R",
                     help="opt-in frame-ring observations (FrameRingBatch, R frames per agent ring); "
                          "default 0: the reference's contiguous (N, 4, 66) stacked obs")
-    ap.add_argument("--persistent", type=int, default=None, metavar="W",
-                    help="ms_step launch shape (SoccerBatch.set_persistent): W waves persistent, 0 one wave per "
-                         "block, -1 one wave per SIMD; default: the library's")
     ap.add_argument("--lane-group", type=int, default=None, metavar="G",
-                    help="ms_step kernel (SoccerBatch.set_lane_group): G = 8 or 16 lanes per env, 0 one lane per "
-                         "env, -1 automatic; default: the library's (8 lanes while envs x 8 fit the SIMDs)")
+                    help="ms_step kernel (SoccerBatch.set_lane_group): G = 2, 8 or 16 lanes per env, 0 one lane "
+                         "per env, -1 automatic; default: the library's (8 lanes while envs x 8 fit the SIMDs, "
+                         "else 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ring-leg", action="store_true", help="skip the frame-ring leg timed beside the headline")
     ap.add_argument("--cpu-envs", type=int, default=65536)
@@ -152,7 +150,7 @@ def regime_key(envs: int, max_steps: int, warmup: int, steps: int) -> str:
 def load_pmc_traffic(key: str, kernel: str):
     """The committed rocprofv3 PMC figures of the step kernel over the same timed window
     (dispatches warmup .. warmup + steps of a run with the same arguments), or None — also when
-    the profiled launch ran another kernel than this run's (lane groups, persistent grid)."""
+    the profiled launch ran another kernel than this run's (lane groups or pairs)."""
     path = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
     try:
         with open(path) as f:
@@ -200,8 +198,6 @@ def main():
         raise SystemExit("--frame-ring and --allgather are exclusive")
     batch = (FrameRingBatch(E, ring=ring, config=cfg, device=dev.index) if ring else
              SoccerBatch(E, config=cfg, device=dev.index))
-    if args.persistent is not None and not ring:
-        batch.set_persistent(args.persistent)
     if args.lane_group is not None and not ring:
         batch.set_lane_group(args.lane_group)
     batch.reset(seed=19 + rank * E)  # env i of rank r seeded 19 + r*E + i (global index)
@@ -382,10 +378,7 @@ def main():
                        "envs_per_gpu": E, "global_envs": world * E, "max_steps": args.max_steps,
                        "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else ""),
                        "launch": (f"lane groups, {batch.lane_group} lanes per env ({64 // batch.lane_group} envs "
-                                  "per wave)" if not ring and batch.lane_group > 0 else
-                                  f"persistent, {batch.persistent_waves} waves" if not ring and
-                                  batch.persistent_waves > 0 and (E + 63) // 64 > batch.persistent_waves
-                                  else "one wave per 64-env block"),
+                                  "per wave)" if not ring and batch.lane_group > 0 else "one wave per 64-env block"),
                        **({"obs_layout": f"frame ring, R = {ring} (opt-in; obs is a strided (N, 4, 66) window)"}
                           if ring else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 2
+#define MS_ABI_VERSION 3
 
 #define MS_N_AGENTS 4
 #define MS_N_BODIES 5 /* 4 agents + ball */
@@ -223,14 +223,6 @@ int ms_reset(ms_env *env, const uint64_t *pcg, const uint8_t *env_mask, int mode
  * ms_stats (read with ms_get_stats, which synchronises). */
 int ms_step(ms_env *env, const float *actions, float *obs, float *rew, uint8_t *term,
             uint8_t *trunc, int8_t *goal, int32_t *score);
-
-/* ms_step's launch shape. waves > 0: when the batch has more 64-env state blocks than that,
- * ms_step runs a persistent grid of `waves` waves, wave w stepping blocks w, w + waves, ...
- * with the first HBM batch of its next block loaded while it steps the current one (same
- * results, bit for bit). waves = 0: one wave per block. waves < 0: one wave per SIMD of the
- * device (4 x compute units), which is ms_create's default. Host-only. */
-int ms_set_persistent(ms_env *env, int waves);
-int ms_get_persistent(const ms_env *env);
 
 /* ms_step's kernel by lanes per env (replaces the serial per-env loop of marl_vecenv.py:39).
  * lanes = 8 or 16: a group of that many lanes steps each env (a wave holds 64 / lanes envs),

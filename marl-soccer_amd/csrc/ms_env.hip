@@ -1368,17 +1368,15 @@ __device__ __forceinline__ void fetch_rest(const DevState& S, int64_t blk, int l
 //      before this step) is staged in LDS;
 //   2. physics; the t-2 snapshot is loaded just before the solver and arrives while it runs;
 //      no other HBM read follows (gfx9 has one vmcnt for loads and stores, so a read after
-//      the stores would wait for them), except PIPE's prefetch of the wave's next block, which
-//      is issued here, before any store of this block, so that it returns while this block's
-//      stores drain;
+//      the stores would wait for them);
 //   3. goal, rewards, outputs, goal respawn, vec auto-reset;
 //   4. frames t-2, t-1, t of agent 0, then agent 1, ... (each 264-B row segment in one burst
 //      of stores), the history slot (t-1 becomes the next step's t-2) and the
 //      state. A lane whose stack is refilled (first step after a reset, or an auto-reset this
 //      step) writes three copies of frame t and the slot instead.
-template <bool RING, bool PIPE>
+template <bool RING>
 __device__ __forceinline__ void step_block(const DevState& S, const Params& P, Lds& L, const int64_t blk, const Fetch& F,
-                                           const int64_t nblk_next, Fetch& N, const float* __restrict__ actions,
+                                           const float* __restrict__ actions,
                                            float* __restrict__ obs, float* __restrict__ rew,
                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
                                            int8_t* __restrict__ goal_out, int32_t* __restrict__ score_out,
@@ -1416,9 +1414,6 @@ __device__ __forceinline__ void step_block(const DevState& S, const Params& P, L
     L.u.np.ch[k][lane] = F.ch[k];
     L.u.np.cj[k][lane] = F.cj[k];
     pk0 |= cache_key(F.ch[k]) << (8 * k);
-  }
-  if constexpr (PIPE) {  // the next block's scalars: their latency hides behind this block's physics
-    if (nblk_next >= 0) fetch_scalars(S, nblk_next, lane, N);
   }
   bool fill3 = false, rng_dirty = false;
   E.rng.shi = F.r0.x; E.rng.slo = F.r0.y;
@@ -1486,9 +1481,6 @@ __device__ __forceinline__ void step_block(const DevState& S, const Params& P, L
     for (int b = 0; b < 5; ++b) { pvx[b] = h1.px[b]; pvy[b] = h1.py[b]; }
     STAMP(7);
     if (ovf) atomicAdd(&ctr->overflow, ovf);
-  }
-  if constexpr (PIPE) {  // the rest of the next block's first batch, ahead of this block's stores
-    if (nblk_next >= 0) fetch_rest(S, nblk_next, lane, actions, N);
   }
   if (active) {
     // goal detection (game.py:401-412)
@@ -1561,11 +1553,8 @@ __device__ __forceinline__ void step_block(const DevState& S, const Params& P, L
   }
 }
 
-// One wave per state block (grid = blocks), or PIPE: a persistent grid of waves, wave w taking
-// blocks w, w + grid, w + 2 grid, ... with the first batch of its next block loaded during the
-// current one (issued before the current block's stores, so it returns while they drain and the
-// next block starts without the start-of-kernel load burst: DESIGN.md §6).
-template <bool RING, bool PIPE>
+// One wave per state block (grid = blocks).
+template <bool RING>
 __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, const float* __restrict__ actions,
                                           float* __restrict__ obs, float* __restrict__ rew,
                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
@@ -1573,26 +1562,12 @@ __device__ __forceinline__ void step_envs(const DevState& S, const Params& P, co
                                           Counters* ctr, const Ring rg) {
   __shared__ Lds L;
   const int lane = threadIdx.x;
-  int64_t blk = blockIdx.x;
+  const int64_t blk = blockIdx.x;
   Fetch F;
   fetch_scalars(S, blk, lane, F);
   fetch_rest(S, blk, lane, actions, F);
   stage_segments(P, L, lane);
-  if constexpr (!PIPE) {
-    step_block<RING, false>(S, P, L, blk, F, -1, F, actions, obs, rew, term, trunc, goal_out, score_out, ctr, rg);
-  } else {
-    const int64_t nblk = (S.n + MS_BLOCK - 1) / MS_BLOCK;
-#pragma unroll 1
-    for (;;) {
-      const int64_t nb = blk + gridDim.x;
-      Fetch N;
-      step_block<RING, true>(S, P, L, blk, F, nb < nblk ? nb : -1, N, actions, obs, rew, term, trunc, goal_out,
-                             score_out, ctr, rg);
-      if (nb >= nblk) break;
-      blk = nb;
-      F = N;
-    }
-  }
+  step_block<RING>(S, P, L, blk, F, actions, obs, rew, term, trunc, goal_out, score_out, ctr, rg);
 }
 
 template <bool DEFAULT_PARAMS>
@@ -1606,28 +1581,9 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_kernel(DevState S, Params Pi
     Params Pd = default_params();
     Pd.max_steps = Pin.max_steps;  // episode length and auto-reset stay runtime values
     Pd.autoreset = Pin.autoreset;
-    step_envs<false, false>(S, Pd, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
+    step_envs<false>(S, Pd, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
   } else {
-    step_envs<false, false>(S, Pin, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
-  }
-}
-
-// ms_step over more blocks than the GPU holds waves at once: a persistent grid, each wave
-// stepping several blocks with its next block's first batch prefetched (step_envs PIPE)
-template <bool DEFAULT_PARAMS>
-__global__ __launch_bounds__(MS_BLOCK) void ms_step_pipe_kernel(DevState S, Params Pin, const float* __restrict__ actions,
-                                                                float* __restrict__ obs, float* __restrict__ rew,
-                                                                uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                                int8_t* __restrict__ goal_out,
-                                                                int32_t* __restrict__ score_out, Counters* ctr) {
-  const Ring none{nullptr, 0, 0, 0};
-  if constexpr (DEFAULT_PARAMS) {
-    Params Pd = default_params();
-    Pd.max_steps = Pin.max_steps;
-    Pd.autoreset = Pin.autoreset;
-    step_envs<false, true>(S, Pd, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
-  } else {
-    step_envs<false, true>(S, Pin, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
+    step_envs<false>(S, Pin, actions, obs, rew, term, trunc, goal_out, score_out, ctr, none);
   }
 }
 
@@ -1642,9 +1598,9 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_ring_kernel(DevState S, Para
     Params Pd = default_params();
     Pd.max_steps = Pin.max_steps;
     Pd.autoreset = Pin.autoreset;
-    step_envs<true, false>(S, Pd, actions, nullptr, rew, term, trunc, goal_out, score_out, ctr, rg);
+    step_envs<true>(S, Pd, actions, nullptr, rew, term, trunc, goal_out, score_out, ctr, rg);
   } else {
-    step_envs<true, false>(S, Pin, actions, nullptr, rew, term, trunc, goal_out, score_out, ctr, rg);
+    step_envs<true>(S, Pin, actions, nullptr, rew, term, trunc, goal_out, score_out, ctr, rg);
   }
 }
 
@@ -1806,7 +1762,6 @@ struct ms_env {
   int device;
   hipStream_t stream;
   int64_t n;
-  int pipe_waves;  // ms_step: > 0 persistent grid of this many waves (0: one wave per block)
   int group;       // ms_step: lanes per env of the lane-group kernel (8 or 16), 0: one lane per env
   int group_solve; // the lane-group kernel's contact-solve schedule (ms_set_group_solve)
   int64_t lanes;   // the device's wave slots at one wave per SIMD x 64 (4 x CUs x 64)
@@ -1986,8 +1941,10 @@ int ms_config_specialised(const ms_config* cfg) {
 static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 
 // ms_step's default kernel: the lane-group kernel (8 lanes per env) while the batch fits the
-// device's SIMDs at one wave each with 8 lanes per env, the one-lane-per-env kernel above that
-static int auto_group(int64_t n, int64_t lanes) { return n * 8 <= lanes ? 8 : 0; }
+// device's SIMDs at one wave each with 8 lanes per env, the lane-pair kernel (two lanes per env,
+// two waves per SIMD) above that — faster than one lane per env at every size measured
+// (16,384-262,144 envs)
+static int auto_group(int64_t n, int64_t lanes) { return n * 8 <= lanes ? 8 : 2; }
 
 int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms_env** out) {
   if (!out || n_envs <= 0) return fail(MS_ERR_INVALID_ARGUMENT, "ms_create: n_envs must be > 0");
@@ -2003,11 +1960,10 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
   if (cfg) h->cfg = *cfg; else ms_config_default(&h->cfg);
   make_params(&h->cfg, &h->P);
   h->default_params = params_are_default(h->P);
-  {  // ms_step's default launch shape: persistent once the batch outgrows one wave per SIMD
+  {  // ms_step's default kernel by batch size (auto_group)
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-    h->pipe_waves = 4 * cus;
-    h->lanes = (int64_t)h->pipe_waves * 64;
+    h->lanes = (int64_t)4 * cus * 64;
     h->group = auto_group(n_envs, h->lanes);
   }
   const size_t n = (size_t)n_envs;
@@ -2134,14 +2090,6 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
         hipLaunchKernelGGL((ms_step_group_kernel<false, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs,
                            rew, term, trunc, goal, score, h->ctr, h->group_solve);
     }
-  } else if (h->pipe_waves > 0 && nblk > (unsigned)h->pipe_waves) {
-    const dim3 grid((unsigned)h->pipe_waves);
-    if (h->default_params)
-      hipLaunchKernelGGL(ms_step_pipe_kernel<true>, grid, dim3(MS_BLOCK), 0, h->stream, h->S, h->P, actions, obs, rew,
-                         term, trunc, goal, score, h->ctr);
-    else
-      hipLaunchKernelGGL(ms_step_pipe_kernel<false>, grid, dim3(MS_BLOCK), 0, h->stream, h->S, h->P, actions, obs,
-                         rew, term, trunc, goal, score, h->ctr);
   } else if (h->default_params) {
     hipLaunchKernelGGL(ms_step_kernel<true>, dim3(nblk), dim3(MS_BLOCK), 0, h->stream, h->S, h->P, actions, obs, rew,
                        term, trunc, goal, score, h->ctr);
@@ -2152,19 +2100,6 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
   HIPCHK(hipGetLastError());
   return MS_OK;
 }
-
-int ms_set_persistent(ms_env* h, int waves) {
-  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_persistent: null handle");
-  if (waves < 0) {  // automatic: one wave per SIMD (four per CU: 39 KB of LDS per wave)
-    int cus = 0;
-    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
-    waves = 4 * cus;
-  }
-  h->pipe_waves = waves;
-  return MS_OK;
-}
-
-int ms_get_persistent(const ms_env* h) { return h ? h->pipe_waves : -1; }
 
 int ms_set_lane_group(ms_env* h, int lanes) {
   if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_lane_group: null handle");
@@ -2191,7 +2126,6 @@ const char* ms_step_kernel_name(const ms_env* h) {
   if (!h) return "";
   if (h->group == 2) return "ms_step_pair_kernel";
   if (h->group > 0) return "ms_step_group_kernel";
-  if (h->pipe_waves > 0 && grid_for(h->n, MS_BLOCK) > (unsigned)h->pipe_waves) return "ms_step_pipe_kernel";
   return "ms_step_kernel";
 }
 

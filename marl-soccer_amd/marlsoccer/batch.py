@@ -324,17 +324,6 @@ class SoccerBatch:
     def reset_stats(self) -> None:
         N.check(self._L.ms_reset_stats(self._h), "ms_reset_stats")
 
-    def set_persistent(self, waves: int = -1) -> None:
-        """ms_step's launch shape (ms_set_persistent): waves > 0 runs a persistent grid of that
-        many waves once the batch has more 64-env blocks than that, each wave stepping several
-        blocks with the next one's loads in flight; 0: one wave per block; -1: one wave per
-        SIMD of the device. Results are identical either way."""
-        N.check(self._L.ms_set_persistent(self._h, int(waves)), "ms_set_persistent")
-
-    @property
-    def persistent_waves(self) -> int:
-        return int(self._L.ms_get_persistent(self._h))
-
     def set_lane_group(self, lanes: int = -1) -> None:
         """ms_step's kernel (ms_set_lane_group): lanes = 8 or 16 steps each env with a group of
         that many lanes (small batches: loads, per-body work, pair tests, prestep and frames

@@ -510,49 +510,6 @@ def test_obs_fallback_for_operands_outside_fast_domain_bitexact(ms, lanes):
     gpu.close()
 
 
-@pytest.mark.parametrize("n,waves", [(1000, 3), (4096, 7), (262144, -1)])
-def test_persistent_launch_bitexact(ms, n, waves):
-    """ms_step as a persistent grid (ms_set_persistent): few waves, each stepping many 64-env
-    blocks (n = 1,000 on 3 waves: 16 blocks, the last one ragged; 4,096 on 7 waves: a wave
-    count that does not divide the 64 blocks; 262,144 on one wave per SIMD, 4 blocks each) with
-    the next block's loads in flight: obs, rewards and the whole state equal the one-wave-per-
-    block launch bit for bit, across goals and auto-resets (max_steps 60), and a subsample
-    equals the fp32 oracle."""
-    steps = 130
-    cfg = cfg_dict(max_steps=60)
-    a = ms.SoccerBatch(n, config=cfg)
-    b = ms.SoccerBatch(n, config=cfg)
-    a.set_persistent(0)
-    b.set_persistent(waves)
-    assert b.persistent_waves > 0 and a.persistent_waves == 0
-    a.reset(seed=19)
-    b.reset(seed=19)
-    sub = np.linspace(0, n - 1, 32).astype(np.int64)
-    ref = orc.OracleBatch(len(sub), "f32", oracle_cfg(a._cfg))
-    ref.reset(np.stack([orc.pcg_from_seed(19 + int(i)) for i in sub]), 0)
-    for t in range(steps):
-        act = sh.hash_actions(n, t)
-        at = torch.from_numpy(act).to(a.device)
-        oa = a.step(at)
-        ob = b.step(at)
-        robs = ref.step(act[sub])[0]
-        if t % 13 == 12 or t == steps - 1:
-            np.testing.assert_array_equal(ob.obs.cpu().numpy(), oa.obs.cpu().numpy(), err_msg=f"obs t={t}")
-            np.testing.assert_array_equal(ob.rew.cpu().numpy(), oa.rew.cpu().numpy(), err_msg=f"rew t={t}")
-            np.testing.assert_array_equal(ob.trunc.cpu().numpy(), oa.trunc.cpu().numpy(), err_msg=f"trunc t={t}")
-            np.testing.assert_array_equal(ob.goal.cpu().numpy(), oa.goal.cpu().numpy(), err_msg=f"goal t={t}")
-            np.testing.assert_array_equal(ob.obs.cpu().numpy()[sub], robs, err_msg=f"oracle obs t={t}")
-    ga, gb = a.export_state(), b.export_state()
-    assert_state_equal(gb, ga, "end")
-    sa, sb = a.stats(), b.stats()
-    assert sb["env_steps"] == sa["env_steps"] == n * steps
-    assert sb["cache_entries_read"] == sa["cache_entries_read"]
-    assert sb["cache_entries_written"] == sa["cache_entries_written"]
-    assert sb["arbiter_overflow"] == 0
-    a.close()
-    b.close()
-
-
 @pytest.mark.parametrize("n,lanes,over,solve", [
     pytest.param(1000, 8, {}, 0, id="1000envs-8lanes"),
     pytest.param(1000, 8, {}, 1, id="1000envs-8lanes-serial"),
@@ -635,7 +592,6 @@ def test_lane_pair_full_size_equals_per_lane(ms, n, max_steps, steps):
     a = ms.SoccerBatch(n, config=cfg)
     b = ms.SoccerBatch(n, config=cfg)
     a.set_lane_group(0)
-    a.set_persistent(0)
     b.set_lane_group(2)
     assert b.step_kernel == "ms_step_pair_kernel" and a.step_kernel == "ms_step_kernel"
     a.reset(seed=19)

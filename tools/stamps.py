@@ -49,7 +49,6 @@ def main():
     ap.add_argument("--every", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=0, help="untimed steps first (1000: steady state)")
     ap.add_argument("--out", default="")
-    ap.add_argument("--persistent", type=int, default=None, help="SoccerBatch.set_persistent(W) (ms_set_persistent)")
     ap.add_argument("--lane-group", type=int, default=None, help="SoccerBatch.set_lane_group(G) (ms_set_lane_group)")
     a, extra = ap.parse_known_args()
     sys.path.insert(0, PKG)
@@ -67,8 +66,6 @@ def main():
     hip = C.CDLL("libamdhip64.so")
     hip.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
     env = SoccerBatch(a.envs, device=0)
-    if a.persistent is not None:
-        env.set_persistent(a.persistent)
     if a.lane_group is not None:
         env.set_lane_group(a.lane_group)
     env.reset(seed=19)
@@ -118,9 +115,7 @@ def main():
                 seg_slow[ORDER[i]].append(d[slow].mean())
     mnc = np.concatenate(maxnc)
     res = {"envs": a.envs, "steps": a.steps, "warmup": a.warmup, "samples": len(totals),
-           "launch": f"lane groups, {env.lane_group} lanes per env" if env.lane_group > 0 else
-                     f"persistent, {env.persistent_waves} waves" if env.persistent_waves > 0 and
-                     (a.envs + 63) // 64 > env.persistent_waves else "one wave per 64-env block",
+           "launch": f"lane groups, {env.lane_group} lanes per env" if env.lane_group > 0 else "one wave per 64-env block",
            "wave_cycles_mean": float(np.mean(totals)), "wave_cycles_slowest5pct": float(np.mean(slow_tot)),
            "launch_span_cycles": float(np.mean(spans)),
            "worst_wave_cycles_mean": float(np.mean([w["cycles"] for w in worst])),

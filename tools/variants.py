@@ -57,7 +57,7 @@ def main():
                 envs = a[i + 1]; i += 2
             elif a[i] == "--steps":
                 steps = a[i + 1]; i += 2
-            elif a[i] in ("--lane-group", "--max-steps", "--warmup", "--persistent"):
+            elif a[i] in ("--lane-group", "--max-steps", "--warmup"):
                 extra += [a[i], a[i + 1]]; i += 2
             else:
                 names.append(a[i]); i += 1
