@@ -1,3 +1,3 @@
-# r04f: the lane-pair kernel (shared static-agent tests): its parity subset, profile at 65,536 envs
-# (bench line, rocprofv3 stats, PMC of both windows), SQ counters and per-phase stamps
-bash tools/gpu.sh multi "parity r04f lane-pair+or+lanes2+or+2lanes+or+ragged+or+lane_pair" "profile r04f --lane-group 2" "sq r04f 65536 --lane-group 2" "stamps r04f G=2 65536 32768"
+# r04f: the whole GPU suite on the lane-pair default; the default bench line's profile at 65,536 envs
+# (rocprofv3 stats, PMC of both windows); the lane-pair kernel's SQ counters and per-phase stamps
+bash tools/gpu.sh multi "suite r04f" "profile r04f" "sq r04f 65536" "stamps r04f G=2 65536 32768"
