@@ -38,7 +38,7 @@ def compiler_usage(tag, kernel):
                 break
         elif cur and kernel in cur and "ILb1E" in cur and v:
             out[k] = v
-    return dict(out, source=f"profiles/{tag}_resource_usage.txt", kernel="ms_step_kernel<true> (default physics)") if out else None
+    return dict(out, source=f"profiles/{tag}_resource_usage.txt", kernel=f"{kernel}<true> (default physics)") if out else None
 
 
 def window_pmc(src, kernel, envs, warmup, steps):
