@@ -70,6 +70,9 @@ def parse():
                          "else 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ring-leg", action="store_true", help="skip the frame-ring leg timed beside the headline")
+    ap.add_argument("--fused", type=int, default=50, metavar="K",
+                    help="N = 1: time ms_step_n (K steps per call, actions given up front) beside the headline "
+                         "(0: skip)")
     ap.add_argument("--cpu-envs", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target wall time of the all-cores CPU baseline (its step count is sized from the "
@@ -325,6 +328,45 @@ def main():
                        "obs": "strided (N, 4, 66) window into a (N, 4, 32, 22) frame ring, same values as obs "
                               "(bench.py --frame-ring 32 gives its roofline line)"}
 
+    # ms_step_n timed beside the headline (N = 1, default run): the same workload with the actions of
+    # K steps handed over per call (an open-loop rollout); with the lane-pair kernel one launch runs
+    # the K steps, each wave stepping its envs back to back. Same envs, seeds and window; its own
+    # pool of uniform actions (one (E, 4, 3) set per step, read from HBM) and its own (K, E, ...)
+    # outputs. Reported as `fused_steps`, never as `value` (the reference's API is one step per call).
+    fused_report = None
+    K = args.fused
+    if world == 1 and not ring and K > 0 and args.steps % K == 0 and args.warmup % K == 0:
+        fb = SoccerBatch(E, config=cfg, device=dev.index)
+        if args.lane_group is not None:
+            fb.set_lane_group(args.lane_group)
+        fb.reset(seed=19)
+        fsets = max(1, min(args.steps // K, int(args.action_gib * (1 << 30) // (E * 48 * K))))
+        fpool = [torch.rand((K, E, 4, 3), device=dev, generator=gen) * 2 - 1 for _ in range(fsets)]
+        fout = {name: torch.empty((K, E) + sh, dtype=dt, device=dev) for name, dt, sh in
+                (("obs", torch.float32, (4, 66)), ("rew", torch.float32, (4,)), ("term", torch.uint8, (4,)),
+                 ("trunc", torch.uint8, (4,)), ("goal", torch.int8, ()), ("score", torch.int32, (2,)))}
+        for i in range(args.warmup // K):
+            fb.step_n(fpool[i % fsets], out=fout)
+        torch.cuda.synchronize()
+        fe0, fe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f0 = time.perf_counter()
+        fe0.record(fb.stream)
+        for i in range(args.steps // K):
+            fb.step_n(fpool[i % fsets], out=fout)
+        fe1.record(fb.stream)
+        torch.cuda.synchronize()
+        f_el = time.perf_counter() - f0
+        f_kern = fe0.elapsed_time(fe1) / args.steps
+        fk = "ms_step_pair_n_kernel" if fb.lane_group == 2 else fb.step_kernel
+        fused_report = {"value": E * args.steps / f_el, "unit": "env-steps/s", "K": K,
+                        "ms_per_step": f_el * 1e3 / args.steps, "kernel": fk, "kernel_ms_per_step": f_kern,
+                        "launches": args.steps // K if fb.lane_group == 2 else args.steps,
+                        "roofline_frac": SURVEY_BYTES * E / (f_kern * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "actions": f"{fsets} distinct (K, E, 4, 3) uniform(-1,1) blocks",
+                        "api": "SoccerBatch.step_n / ms_step_n: K steps with the actions given up front"}
+        fb.close()
+        del fpool, fout
+
     # arbiter-cache entries per env-step read and written by the timed launches themselves
     # (the kernel's per-block tally, ms_stats): the cache term of the algorithmic byte count
     steps_counted = max(1, stats["env_steps"])
@@ -410,6 +452,8 @@ def main():
             line["with_obs_allgather"] = gather_report
         if ring_report is not None:
             line["frame_ring"] = ring_report
+        if fused_report is not None:
+            line["fused_steps"] = fused_report
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args)
             cb["gpu_over_cpu"] = value / cb["value"]

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 3
+#define MS_ABI_VERSION 4
 
 #define MS_N_AGENTS 4
 #define MS_N_BODIES 5 /* 4 agents + ball */
@@ -223,6 +223,18 @@ int ms_reset(ms_env *env, const uint64_t *pcg, const uint8_t *env_mask, int mode
  * ms_stats (read with ms_get_stats, which synchronises). */
 int ms_step(ms_env *env, const float *actions, float *obs, float *rew, uint8_t *term,
             uint8_t *trunc, int8_t *goal, int32_t *score);
+
+/* K consecutive ms_step calls with actions given up front (open loop: a random-action or
+ * scripted rollout, the workload of marl_vecenv.py:30-68 driven by pre-drawn actions) (ABI 4).
+ * actions [K][N][4][3]; every output with a leading K dimension: obs [K][N][4][66],
+ * rew [K][N][4], term / trunc [K][N][4], goal [K][N], score [K][N][2] (NULL: not written; obs
+ * required). Results are those of K ms_step calls, bit for bit. With the lane-pair kernel
+ * (ms_set_lane_group(2), the default from 16,384 envs) the K steps run in ONE launch, each wave
+ * stepping its 32 envs K times back to back (a wave slowed by a pile-up in one step no longer
+ * holds the whole grid at every step boundary); other launch shapes issue K ms_step launches.
+ * 1 <= K, alignment as ms_step; MS_ERR_INVALID_ARGUMENT otherwise. */
+int ms_step_n(ms_env *env, int K, const float *actions, float *obs, float *rew, uint8_t *term,
+              uint8_t *trunc, int8_t *goal, int32_t *score);
 
 /* ms_step's kernel by lanes per env (replaces the serial per-env loop of marl_vecenv.py:39).
  * lanes = 8 or 16: a group of that many lanes steps each env (a wave holds 64 / lanes envs),

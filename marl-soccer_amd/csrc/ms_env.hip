@@ -2101,6 +2101,35 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
   return MS_OK;
 }
 
+int ms_step_n(ms_env* h, int K, const float* actions, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
+              int8_t* goal, int32_t* score) {
+  if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_n: null handle");
+  if (K < 1) return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_n: K < 1");
+  if (!actions || !obs) return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_n: actions and obs are required");
+  if (((uintptr_t)actions & 15u) || ((uintptr_t)obs & 7u) || ((uintptr_t)rew & 15u) || ((uintptr_t)term & 3u) ||
+      ((uintptr_t)trunc & 3u) || ((uintptr_t)score & 7u))
+    return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_n: misaligned buffer (actions/rew 16 B, obs/score 8 B, flags 4 B)");
+  if (h->group == 2) {
+    const dim3 grid(grid_for(h->n, pr::EPW));
+    if (h->default_params)
+      hipLaunchKernelGGL(ms_step_pair_n_kernel<true>, grid, dim3(64), 0, h->stream, h->S, h->P, K, actions, obs, rew,
+                         term, trunc, goal, score, h->ctr);
+    else
+      hipLaunchKernelGGL(ms_step_pair_n_kernel<false>, grid, dim3(64), 0, h->stream, h->S, h->P, K, actions, obs, rew,
+                         term, trunc, goal, score, h->ctr);
+    HIPCHK(hipGetLastError());
+    return MS_OK;
+  }
+  const int64_t n = h->n;
+  for (int k = 0; k < K; ++k) {
+    const int64_t o = (int64_t)k * n;
+    const int rc = ms_step(h, actions + o * 12, obs + o * 264, rew ? rew + o * 4 : nullptr, term ? term + o * 4 : nullptr,
+                           trunc ? trunc + o * 4 : nullptr, goal ? goal + o : nullptr, score ? score + o * 2 : nullptr);
+    if (rc != MS_OK) return rc;
+  }
+  return MS_OK;
+}
+
 int ms_set_lane_group(ms_env* h, int lanes) {
   if (!h) return fail(MS_ERR_INVALID_ARGUMENT, "ms_set_lane_group: null handle");
   if (lanes < 0) lanes = auto_group(h->n, h->lanes);

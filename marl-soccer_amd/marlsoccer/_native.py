@@ -71,7 +71,7 @@ EXPORTED = (
     "ms_config_default", "ms_create", "ms_destroy", "ms_set_stream", "ms_num_envs", "ms_seed_pcg64",
     "ms_seed_pcg64_range", "ms_reset", "ms_step", "ms_observe", "ms_export_state", "ms_import_state",
     "ms_debug_rewards", "ms_get_stats", "ms_reset_stats", "ms_last_error", "ms_abi_version",
-    "ms_config_specialised", "ms_step_ring", "ms_reset_ring",
+    "ms_config_specialised", "ms_step_ring", "ms_reset_ring", "ms_step_n",
     "ms_set_lane_group", "ms_get_lane_group", "ms_set_group_solve", "ms_get_group_solve", "ms_step_kernel_name",
     "ms_policy_forward", "ms_policy_last_error", "ms_policy_run", "ms_rollout_record",
 )
@@ -125,6 +125,9 @@ def lib():
         L.ms_step_ring.restype = C.c_int
         L.ms_reset_ring.argtypes = [P, P, P, C.c_int, P, C.c_int, C.c_int]
         L.ms_reset_ring.restype = C.c_int
+    if hasattr(L, "ms_step_n"):  # likewise (ABI 4)
+        L.ms_step_n.argtypes = [P, C.c_int, P, P, P, P, P, P, P]
+        L.ms_step_n.restype = C.c_int
     if hasattr(L, "ms_set_lane_group"):  # likewise
         L.ms_set_lane_group.argtypes = [P, C.c_int]
         L.ms_set_lane_group.restype = C.c_int

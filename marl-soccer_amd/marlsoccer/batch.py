@@ -211,6 +211,39 @@ class SoccerBatch:
             self.raise_if_nonfinite(actions)
         return StepOutput((self.obs, self.rew, self.term, self.trunc, self.goal, self.score))
 
+    def step_n(self, actions: torch.Tensor, out: dict | None = None) -> StepOutput:
+        """K consecutive steps with the actions given up front (ms_step_n): actions (K, N, 4, 3)
+        float32 on the env's device, e.g. a random-action rollout. Returns the K steps' outputs
+        with a leading K dimension (obs (K, N, 4, 66), rew (K, N, 4), term / trunc (K, N, 4),
+        goal (K, N), score (K, N, 2)); `out` may hold any of those tensors to write into. Bit for
+        bit what K step() calls return; with the lane-pair kernel the K steps are one launch."""
+        if actions.dim() != 4 or actions.shape[1:] != (self.num_envs, 4, 3):
+            raise ValueError(f"actions must have shape (K, {self.num_envs}, 4, 3), got {tuple(actions.shape)}")
+        K = int(actions.shape[0])
+        if K < 1:
+            raise ValueError("step_n: K >= 1 steps")
+        if actions.dtype != torch.float32:
+            actions = actions.float()
+        if actions.device != self.device:
+            raise ValueError(f"tensor on {actions.device}, env on {self.device}")
+        actions = actions.contiguous()
+        o = dict(out or {})
+        n, dev = self.num_envs, self.device
+        for name, dt, sh in OUTPUT_LAYOUT:
+            t = o.get(name)
+            if t is None:
+                o[name] = torch.empty((K, n) + sh, dtype=dt, device=dev)
+            elif t.shape != (K, n) + sh or t.dtype != dt or t.device != dev or not t.is_contiguous():
+                raise ValueError(f"out[{name!r}] must be a contiguous {dt} tensor of shape {(K, n) + sh} on {dev}")
+        with torch.cuda.device(self.device):
+            cur = self._enter()
+            rc = self._L.ms_step_n(self._h, K, self._ptr(actions), self._ptr(o["obs"]), self._ptr(o["rew"]),
+                                   self._ptr(o["term"]), self._ptr(o["trunc"]), self._ptr(o["goal"]),
+                                   self._ptr(o["score"]))
+            self._leave(cur, actions)
+        N.check(rc, "ms_step_n")
+        return StepOutput((o["obs"], o["rew"], o["term"], o["trunc"], o["goal"], o["score"]))
+
     def raise_if_nonfinite(self, actions: torch.Tensor | None = None) -> None:
         """Raise the reference's ValueError (soccer_env.py:116-117) if any env was handed a
         non-finite action since the last check (synchronises the env's stream), then clear

@@ -71,7 +71,7 @@ profile() {
   for WS in "5 20" "1000 1000"; do
     read W S <<< "$WS"
     for C in FETCH_SIZE WRITE_SIZE; do
-      timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_${C}_w${W}_s${S} -o run -- python bench.py --warmup $W --steps $S --no-cpu-baseline --no-ring-leg "$@" > $O/pmc_${C}_w${W}_s${S}.log 2>&1 \
+      timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_${C}_w${W}_s${S} -o run -- python bench.py --warmup $W --steps $S --no-cpu-baseline --no-ring-leg --fused 0 "$@" > $O/pmc_${C}_w${W}_s${S}.log 2>&1 \
         || { echo "pmc $C w$W s$S failed"; tail -20 $O/pmc_${C}_w${W}_s${S}.log; return 1; }
     done
   done
@@ -86,7 +86,7 @@ sq() {  # tag envs bench-args...
   local i=0 P
   for P in "$P1" "$P2" "$P3"; do
     i=$((i+1))
-    timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- python bench.py --envs $N --warmup 1000 --steps 100 --no-cpu-baseline --no-ring-leg "$@" > $O/p$i.log 2>&1 \
+    timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- python bench.py --envs $N --warmup 1000 --steps 100 --no-cpu-baseline --no-ring-leg --fused 0 "$@" > $O/p$i.log 2>&1 \
       || { echo "sq pass $i failed"; tail -5 $O/p$i.log; return 1; }
   done
   python tools/sq_summary.py $O --last 100 --json $O/summary.json | tee $O/summary.txt

@@ -63,7 +63,7 @@ def main():
                 names.append(a[i]); i += 1
         for name in names:
             env = dict(os.environ, MARL_SOCCER_LIB=os.path.join(VDIR, f"lib_{name}.so"))
-            r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-ring-leg", "--envs", envs,
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-ring-leg", "--fused", "0", "--envs", envs,
                                 "--steps", steps, *extra], env=env, capture_output=True, text=True, timeout=300)
             if r.returncode != 0:
                 print(name, "FAILED", r.stderr[-2000:], flush=True)
