@@ -26,9 +26,9 @@ NS = 24  # MS_NSTAMP
 ACC = {16: "AA test", 17: "AA insert", 18: "AA iterations", 19: "SA test", 20: "SA insert", 21: "SA iterations"}
 
 # (label, from, to) in kernel order; a stamp inside a branch no lane took is carried forward
-ORDER = [0, 1, 2, 11, 13, 3, 14, 4, 23, 15, 22, 5, 6, 7, 8, 9, 10]
+ORDER = [0, 1, 2, 11, 13, 3, 14, 4, 15, 22, 5, 6, 7, 8, 9, 10]
 LABELS = {1: "load+actions", 2: "integrate+transforms", 11: "bp+nphase AA/BA", 13: "nphase static-agent",
-          3: "nphase ball-wall+cache age", 14: "prestep", 4: "velocity", 23: "early frames t-2, t-1 (lane pairs)", 15: "warm start",
+          3: "nphase ball-wall+cache age", 14: "prestep", 4: "velocity", 15: "warm start",
           22: "solver schedule (lane groups)", 5: "solver x10",
           6: "cache write", 7: "meta", 8: "goal+reward+outputs", 9: "obs frames+snap", 10: "state stores"}
 
