@@ -348,6 +348,7 @@ def main():
         for i in range(args.warmup // K):
             fb.step_n(fpool[i % fsets], out=fout)
         torch.cuda.synchronize()
+        fb.reset_stats()
         fe0, fe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         f0 = time.perf_counter()
         fe0.record(fb.stream)
@@ -358,12 +359,27 @@ def main():
         f_el = time.perf_counter() - f0
         f_kern = fe0.elapsed_time(fe1) / args.steps
         fk = "ms_step_pair_n_kernel" if fb.lane_group == 2 else fb.step_kernel
+        fst = fb.stats()
+        f_arb = 0.5 * (fst["cache_entries_read"] + fst["cache_entries_written"]) / max(1, fst["env_steps"])
+        f_bytes = SURVEY_BYTES + 2 * ARB_BYTES * f_arb
+        f_ach = f_bytes * E / (f_kern * 1e-3) / 1e9
+        # HBM bytes per env-step of the committed rocprofv3 PMC passes over this kernel (same E, K)
+        f_traffic, f_src = None, None
+        pf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04k", "pmc_fused.json")
+        if os.path.exists(pf):
+            pm = json.load(open(pf))
+            if pm.get("envs") == E and pm.get("K") == K and pm.get("kernel", "").startswith(fk):
+                f_traffic = pm["hbm_bytes_per_env_step"] * E / (f_kern * 1e-3) / 1e9
+                f_src = "profiles/r04k/pmc_fused.json (FETCH_SIZE x 2 + WRITE_SIZE per env-step) over this run's time"
         fused_report = {"value": E * args.steps / f_el, "unit": "env-steps/s", "K": K,
                         "ms_per_step": f_el * 1e3 / args.steps, "kernel": fk, "kernel_ms_per_step": f_kern,
                         "launches": args.steps // K if fb.lane_group == 2 else args.steps,
-                        "roofline_frac": SURVEY_BYTES * E / (f_kern * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "roofline": {"bound": "hbm", "achieved": f_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": f_ach / HBM_PEAK_GBS, "traffic": f_traffic, "traffic_source": f_src,
+                                     "alg_bytes_per_env_step": f_bytes},
+                        "arbiter_overflow": fst["arbiter_overflow"],
                         "actions": f"{fsets} distinct (K, E, 4, 3) uniform(-1,1) blocks",
-                        "api": "SoccerBatch.step_n / ms_step_n: K steps with the actions given up front"}
+                        "api": "SoccerBatch.step_n / ms_step_n: K steps with the actions given up front (open loop)"}
         fb.close()
         del fpool, fout
 
