@@ -358,7 +358,8 @@ def main():
         torch.cuda.synchronize()
         f_el = time.perf_counter() - f0
         f_kern = fe0.elapsed_time(fe1) / args.steps
-        fk = "ms_step_pair_n_kernel" if fb.lane_group == 2 else fb.step_kernel
+        fk = {"ms_step_pair_kernel": "ms_step_pair_n_kernel", "ms_step_group_kernel": "ms_step_group_n_kernel"}.get(
+            fb.step_kernel, fb.step_kernel)
         fst = fb.stats()
         f_arb = 0.5 * (fst["cache_entries_read"] + fst["cache_entries_written"]) / max(1, fst["env_steps"])
         f_bytes = SURVEY_BYTES + 2 * ARB_BYTES * f_arb
@@ -373,7 +374,7 @@ def main():
                 f_src = "profiles/r04k/pmc_fused.json (FETCH_SIZE x 2 + WRITE_SIZE per env-step) over this run's time"
         fused_report = {"value": E * args.steps / f_el, "unit": "env-steps/s", "K": K,
                         "ms_per_step": f_el * 1e3 / args.steps, "kernel": fk, "kernel_ms_per_step": f_kern,
-                        "launches": args.steps // K if fb.lane_group == 2 else args.steps,
+                        "launches": args.steps // K if fb.lane_group > 0 else args.steps,
                         "roofline": {"bound": "hbm", "achieved": f_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                      "frac": f_ach / HBM_PEAK_GBS, "traffic": f_traffic, "traffic_source": f_src,
                                      "alg_bytes_per_env_step": f_bytes},

@@ -228,10 +228,11 @@ int ms_step(ms_env *env, const float *actions, float *obs, float *rew, uint8_t *
  * scripted rollout, the workload of marl_vecenv.py:30-68 driven by pre-drawn actions) (ABI 4).
  * actions [K][N][4][3]; every output with a leading K dimension: obs [K][N][4][66],
  * rew [K][N][4], term / trunc [K][N][4], goal [K][N], score [K][N][2] (NULL: not written; obs
- * required). Results are those of K ms_step calls, bit for bit. With the lane-pair kernel
- * (ms_set_lane_group(2), the default from 16,384 envs) the K steps run in ONE launch, each wave
- * stepping its 32 envs K times back to back (a wave slowed by a pile-up in one step no longer
- * holds the whole grid at every step boundary); other launch shapes issue K ms_step launches.
+ * required). Results are those of K ms_step calls, bit for bit. With the lane-pair and the
+ * lane-group kernels (ms_set_lane_group 2, 8, 16: the defaults) the K steps run in ONE launch,
+ * each wave stepping its envs K times back to back (a wave slowed by a pile-up in one step no
+ * longer holds the whole grid at every step boundary); the one-lane-per-env kernel (lanes 0)
+ * issues K ms_step launches.
  * 1 <= K, alignment as ms_step; MS_ERR_INVALID_ARGUMENT otherwise. */
 int ms_step_n(ms_env *env, int K, const float *actions, float *obs, float *rew, uint8_t *term,
               uint8_t *trunc, int8_t *goal, int32_t *score);

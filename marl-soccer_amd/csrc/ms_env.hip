@@ -2120,6 +2120,27 @@ int ms_step_n(ms_env* h, int K, const float* actions, float* obs, float* rew, ui
     HIPCHK(hipGetLastError());
     return MS_OK;
   }
+  if (h->group > 0) {
+    const int G = h->group;
+    const dim3 grid(grid_for(h->n, 64 / G));
+    if (G == 8) {
+      if (h->default_params)
+        hipLaunchKernelGGL((ms_step_group_n_kernel<true, 8>), grid, dim3(64), 0, h->stream, h->S, h->P, K, actions, obs,
+                           rew, term, trunc, goal, score, h->ctr, h->group_solve);
+      else
+        hipLaunchKernelGGL((ms_step_group_n_kernel<false, 8>), grid, dim3(64), 0, h->stream, h->S, h->P, K, actions,
+                           obs, rew, term, trunc, goal, score, h->ctr, h->group_solve);
+    } else {
+      if (h->default_params)
+        hipLaunchKernelGGL((ms_step_group_n_kernel<true, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, K, actions,
+                           obs, rew, term, trunc, goal, score, h->ctr, h->group_solve);
+      else
+        hipLaunchKernelGGL((ms_step_group_n_kernel<false, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, K, actions,
+                           obs, rew, term, trunc, goal, score, h->ctr, h->group_solve);
+    }
+    HIPCHK(hipGetLastError());
+    return MS_OK;
+  }
   const int64_t n = h->n;
   for (int k = 0; k < K; ++k) {
     const int64_t o = (int64_t)k * n;

@@ -216,7 +216,8 @@ class SoccerBatch:
         float32 on the env's device, e.g. a random-action rollout. Returns the K steps' outputs
         with a leading K dimension (obs (K, N, 4, 66), rew (K, N, 4), term / trunc (K, N, 4),
         goal (K, N), score (K, N, 2)); `out` may hold any of those tensors to write into. Bit for
-        bit what K step() calls return; with the lane-pair kernel the K steps are one launch."""
+        bit what K step() calls return; with the lane-pair and lane-group kernels (the defaults) the K
+        steps are one launch."""
         if actions.dim() != 4 or actions.shape[1:] != (self.num_envs, 4, 3):
             raise ValueError(f"actions must have shape (K, {self.num_envs}, 4, 3), got {tuple(actions.shape)}")
         K = int(actions.shape[0])

@@ -1,8 +1,8 @@
 """ms_step_n (SoccerBatch.step_n): K steps with the actions given up front. With the lane-pair
-kernel the K steps are ONE launch (ms_step_pair_n_kernel: each wave steps its envs K times back
-to back); with the other launch shapes K ms_step launches. Either way the results must be those of
-K ms_step calls, bit for bit, and those of the fp32 oracle (marl_vecenv.py:30-68 driven by a
-pre-drawn action sequence)."""
+and lane-group kernels the K steps are ONE launch (ms_step_pair_n_kernel / ms_step_group_n_kernel:
+each wave steps its envs K times back to back); with the one-lane-per-env kernel K ms_step
+launches. Either way the results must be those of K ms_step calls, bit for bit, and those of the
+fp32 oracle (marl_vecenv.py:30-68 driven by a pre-drawn action sequence)."""
 import numpy as np
 import pytest
 
@@ -37,7 +37,7 @@ def chase_sequence(ref, n, K, rng, chaser):
     return np.stack(acts), outs
 
 
-@pytest.mark.parametrize("lanes", [2, 0, 8], ids=["lane-pair-fused", "per-lane", "lanes8"])
+@pytest.mark.parametrize("lanes", [2, 8, 16, 0], ids=["lane-pair-fused", "lanes8-fused", "lanes16-fused", "per-lane"])
 @pytest.mark.parametrize("n", [1000, 4096])
 def test_step_n_chase_bitexact_vs_oracle(ms, lanes, n):
     """Three step_n calls of K = 48 under the chase policy (episodes of 60 steps: auto-resets

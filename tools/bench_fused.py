@@ -58,7 +58,7 @@ def main():
             el = time.perf_counter() - t0
             kms = e0.elapsed_time(e1) / a.steps
             print(json.dumps({"envs": E, "K": K, "max_steps": a.max_steps, "kernel": b.step_kernel.replace(
-                "ms_step_pair_kernel", "ms_step_pair_n_kernel"), "us_per_step": kms * 1e3,
+                "_kernel", "_n_kernel") if b.lane_group > 0 else b.step_kernel, "us_per_step": kms * 1e3,
                 "env_steps_per_s": E * a.steps / el, "wall_us_per_step": el * 1e6 / a.steps}), flush=True)
             b.close()
             del pool, out
