@@ -135,6 +135,13 @@ class SyncMultiAgentVecEnv:
         (obs, rew f32, term u8, trunc u8, goal i8, score i32), overwritten by the next step."""
         return self.batch.step(actions)
 
+    def step_n_tensors(self, actions):
+        """K steps with the actions given up front (open loop: random or scripted actions):
+        actions torch float32 (K, N, 4, 3) on the env's device; returns the K steps' device
+        tensors with a leading K dimension, bit-identical to K step_tensors calls (one launch
+        for the default kernels: SoccerBatch.step_n, ms_step_n)."""
+        return self.batch.step_n(actions)
+
     def _dict_to_array(self, data_dict):
         return np.array([data_dict[a] for a in self.possible_agents])
 

@@ -109,3 +109,23 @@ def test_step_n_rejects_bad_arguments(ms):
     with pytest.raises(ValueError):
         gpu.step_n(torch.zeros((2, 64, 4, 3), device=gpu.device), out={"obs": torch.zeros((1, 64, 4, 66), device=gpu.device)})
     gpu.close()
+
+
+def test_vec_env_step_n_tensors_matches_oracle(ms):
+    """The vec-env wrapper's open-loop entry (SyncMultiAgentVecEnv.step_n_tensors, marl_vecenv.py's
+    step driven by pre-drawn uniform actions) against the fp32 oracle step by step."""
+    from marl_vecenv import SyncMultiAgentVecEnv
+    from soccer_env import soccerenv
+    n, K = 16, 40
+    envs = SyncMultiAgentVecEnv([lambda: soccerenv() for _ in range(n)])
+    envs.reset(seed=19)
+    ref = orc.OracleBatch(n, "f32")
+    ref.reset(np.stack([orc.pcg_from_seed(19 + i) for i in range(n)]), 0)
+    act = np.random.default_rng(3).uniform(-1, 1, (K, n, 4, 3)).astype(np.float32)
+    res = envs.step_n_tensors(torch.from_numpy(act).to(envs.batch.device))
+    obs, rew = res.obs.cpu().numpy(), res.rew.cpu().numpy()
+    for k in range(K):
+        r_obs, r_rew = ref.step(act[k])[:2]
+        np.testing.assert_array_equal(obs[k], r_obs, err_msg=f"obs step {k}")
+        np.testing.assert_array_equal(rew[k], r_rew.astype(np.float32), err_msg=f"rew step {k}")
+    envs.close()
