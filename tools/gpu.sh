@@ -9,6 +9,7 @@
 #                                               passes over the driver's and the default window
 #   tools/gpu.sh configs  <tag>                 the BASELINE configs' per-GPU batch sizes
 #   tools/gpu.sh sq       <tag> <envs> [bench args]  SQ counter passes (steady window: warm-up 1000, 100 steps)
+#   tools/gpu.sh sqfused  <tag> <envs> <K>      SQ counter passes over the K-step launch (10 timed launches)
 #   tools/gpu.sh stamps   <tag> [G=lanes] <envs...>  per-phase wave stamps (tools/stamps.py; stamps library prebuilt)
 #   tools/gpu.sh rehearse <tag>                 bench.py --gpus 2 with both ranks on cuda:0 (gloo), 2 x 8,192 and 2 x 65,536
 #   tools/gpu.sh policy   <tag>                 policy/rollout GPU tests + bench_policy + graph rollouts
@@ -91,6 +92,22 @@ sq() {  # tag envs bench-args...
   done
   python tools/sq_summary.py $O --last 100 --json $O/summary.json | tee $O/summary.txt
   rm -rf $O/p1 $O/p2 $O/p3  # the raw per-dispatch CSVs exceed gpurun's 64-MiB copy-back
+}
+
+sqfused() {  # tag envs K: the SQ passes over the open-loop K-step launch (tools/bench_fused.py)
+  local T=$1 N=$2 K=$3
+  local O=gpurun_out/$T/sqfused_$N; mkdir -p $O
+  local P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
+  local P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_VMEM SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH"
+  local P3="SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_INSTS"
+  local i=0 P
+  for P in "$P1" "$P2" "$P3"; do
+    i=$((i+1))
+    timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- python tools/bench_fused.py --envs $N --k $K --steps $((10 * K)) --warmup $((10 * K)) > $O/p$i.log 2>&1 \
+      || { echo "sqfused pass $i failed"; tail -5 $O/p$i.log; return 1; }
+  done
+  python tools/sq_summary.py $O --last 10 --json $O/summary.json | tee $O/summary.txt
+  rm -rf $O/p1 $O/p2 $O/p3
 }
 
 stamps() {  # tag [G=lanes] envs...

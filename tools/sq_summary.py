@@ -4,7 +4,7 @@
     python tools/sq_summary.py <dir> [--last K] [--json out.json]
 
 Each pass directory <dir>/p*/ holds one rocprofv3 counter_collection.csv. Every step-kernel
-dispatch (ms_step_kernel, ms_step_pipe_kernel, ms_step_group_kernel, ms_step_pair_kernel) is a
+dispatch (ms_step_kernel, ms_step_group_kernel, ms_step_pair_kernel and the K-step *_n_kernel launches) is a
 row group; the last K dispatches of the step kernel (the bench's timed window) are kept and the
 median of each counter over them is reported, per dispatch and per wave. SQ cycle counters are
 quad-cycles (x4 = clock cycles). WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES.
@@ -16,7 +16,8 @@ import json
 import statistics
 from collections import defaultdict
 
-STEP = ("ms_step_kernel", "ms_step_pipe_kernel", "ms_step_group_kernel", "ms_step_pair_kernel")
+STEP = ("ms_step_kernel", "ms_step_pipe_kernel", "ms_step_group_kernel", "ms_step_pair_kernel",
+        "ms_step_pair_n_kernel", "ms_step_group_n_kernel")
 
 
 def main():
