@@ -10,6 +10,8 @@
 #   tools/gpu.sh configs  <tag>                 the BASELINE configs' per-GPU batch sizes
 #   tools/gpu.sh sq       <tag> <envs> [bench args]  SQ counter passes (steady window: warm-up 1000, 100 steps)
 #   tools/gpu.sh sqfused  <tag> <envs> <K>      SQ counter passes over the K-step launch (10 timed launches)
+#   tools/gpu.sh fused    <tag> "envs..." "K..."  K-step launch sweep (tools/bench_fused.py)
+#   tools/gpu.sh pmcfused <tag> <envs> <K>      FETCH/WRITE PMC passes + kernel trace over the K-step launch
 #   tools/gpu.sh stamps   <tag> [G=lanes] <envs...>  per-phase wave stamps (tools/stamps.py; stamps library prebuilt)
 #   tools/gpu.sh rehearse <tag>                 bench.py --gpus 2 with both ranks on cuda:0 (gloo), 2 x 8,192 and 2 x 65,536
 #   tools/gpu.sh policy   <tag>                 policy/rollout GPU tests + bench_policy + graph rollouts
@@ -92,6 +94,23 @@ sq() {  # tag envs bench-args...
   done
   python tools/sq_summary.py $O --last 100 --json $O/summary.json | tee $O/summary.txt
   rm -rf $O/p1 $O/p2 $O/p3  # the raw per-dispatch CSVs exceed gpurun's 64-MiB copy-back
+}
+
+fused() {  # tag "envs..." "K...": tools/bench_fused.py sweep (open-loop K-step launch), steady window
+  local O=gpurun_out/$1; mkdir -p $O
+  timeout -k 10 400 python tools/bench_fused.py --envs $2 --k $3 >> $O/fused.jsonl 2>> $O/fused.err || { tail -5 $O/fused.err; return 1; }
+  cat $O/fused.jsonl
+}
+
+pmcfused() {  # tag envs K: FETCH_SIZE / WRITE_SIZE passes and a kernel-trace run over the K-step launch
+  local T=$1 N=$2 K=$3 C
+  local O=gpurun_out/$T; mkdir -p $O
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 240 rocprofv3 --pmc $C --output-format csv -d $O/pmc_fused_$C -o run -- python tools/bench_fused.py --envs $N --k $K > $O/pmc_fused_$C.log 2>&1 \
+      || { echo "pmc $C failed"; tail -5 $O/pmc_fused_$C.log; return 1; }
+  done
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_fused -o run -- python tools/bench_fused.py --envs $N --k $K > $O/trace_fused.log 2>&1 \
+    || { echo "trace failed"; tail -5 $O/trace_fused.log; return 1; }
 }
 
 sqfused() {  # tag envs K: the SQ passes over the open-loop K-step launch (tools/bench_fused.py)
