@@ -129,3 +129,37 @@ def test_vec_env_step_n_tensors_matches_oracle(ms):
         np.testing.assert_array_equal(obs[k], r_obs, err_msg=f"obs step {k}")
         np.testing.assert_array_equal(rew[k], r_rew.astype(np.float32), err_msg=f"rew step {k}")
     envs.close()
+
+
+@pytest.mark.parametrize("lanes", [2, 8], ids=["lane-pair-fused", "lanes8-fused"])
+def test_step_n_nonfinite_actions_skip_like_step(ms, lanes):
+    """A non-finite action inside a K-step launch skips that env for that step only (reward NaN,
+    state untouched; soccer_env.py:101-117's check, counted in ms_stats), exactly as the same
+    action sequence through K step() calls does."""
+    n, K = 256, 12
+    a = ms.SoccerBatch(n)
+    b = ms.SoccerBatch(n)
+    a.set_lane_group(lanes)
+    b.set_lane_group(lanes)
+    a.reset(seed=7)
+    b.reset(seed=7)
+    gen = torch.Generator(device=a.device)
+    gen.manual_seed(11)
+    acts = torch.rand((K, n, 4, 3), generator=gen, device=a.device) * 2.0 - 1.0
+    acts[3, 5, 1, 0] = float("nan")
+    acts[3, 200, 3, 2] = float("inf")
+    acts[7, 5, 0, 1] = float("-inf")
+    res = b.step_n(acts)
+    for k in range(K):
+        o = a.step(acts[k])
+        for f in ("obs", "term", "trunc", "goal", "score"):
+            assert torch.equal(getattr(o, f), getattr(res, f)[k]), f"{f} step {k}"
+        # rewards bit for bit, NaN included
+        assert torch.equal(o.rew.view(torch.int32), res.rew[k].view(torch.int32)), f"rew step {k}"
+    assert torch.isnan(res.rew[3, 5]).any() and torch.isnan(res.rew[3, 200]).any() and torch.isnan(res.rew[7, 5]).any()
+    assert not torch.isnan(res.rew[4]).any()
+    assert_state_equal(b.export_state(), a.export_state(), "end")
+    sa, sb = a.stats(), b.stats()
+    assert sa["nonfinite_envs"] == sb["nonfinite_envs"] == 3
+    a.close()
+    b.close()
