@@ -232,7 +232,10 @@ int ms_step(ms_env *env, const float *actions, float *obs, float *rew, uint8_t *
  * lane-group kernels (ms_set_lane_group 2, 8, 16: the defaults) the K steps run in ONE launch,
  * each wave stepping its envs K times back to back (a wave slowed by a pile-up in one step no
  * longer holds the whole grid at every step boundary); the one-lane-per-env kernel (lanes 0)
- * issues K ms_step launches.
+ * issues K ms_step launches. An env whose actions at step k are not all finite is skipped for
+ * that step exactly as ms_step skips it: counted in ms_stats, its step-k reward NaN, and its other
+ * step-k outputs not written (ms_step's batch buffer keeps the previous values; here the caller's
+ * K-step slot keeps what it held).
  * 1 <= K, alignment as ms_step; MS_ERR_INVALID_ARGUMENT otherwise. */
 int ms_step_n(ms_env *env, int K, const float *actions, float *obs, float *rew, uint8_t *term,
               uint8_t *trunc, int8_t *goal, int32_t *score);
