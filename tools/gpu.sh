@@ -10,7 +10,7 @@
 #   tools/gpu.sh configs  <tag>                 the BASELINE configs' per-GPU batch sizes
 #   tools/gpu.sh sq       <tag> <envs> [bench args]  SQ counter passes (steady window: warm-up 1000, 100 steps)
 #   tools/gpu.sh sqfused  <tag> <envs> <K>      SQ counter passes over the K-step launch (10 timed launches)
-#   tools/gpu.sh fused    <tag> "envs..." "K..."  K-step launch sweep (tools/bench_fused.py)
+#   tools/gpu.sh fused    <tag> <envs> <K>       K-step launch sweep (tools/bench_fused.py; "+" joins values)
 #   tools/gpu.sh pmcfused <tag> <envs> <K>      FETCH/WRITE PMC passes + kernel trace over the K-step launch
 #   tools/gpu.sh stamps   <tag> [G=lanes] <envs...>  per-phase wave stamps (tools/stamps.py; stamps library prebuilt)
 #   tools/gpu.sh rehearse <tag>                 bench.py --gpus 2 with both ranks on cuda:0 (gloo), 2 x 8,192 and 2 x 65,536
@@ -96,9 +96,9 @@ sq() {  # tag envs bench-args...
   rm -rf $O/p1 $O/p2 $O/p3  # the raw per-dispatch CSVs exceed gpurun's 64-MiB copy-back
 }
 
-fused() {  # tag "envs..." "K...": tools/bench_fused.py sweep (open-loop K-step launch), steady window
+fused() {  # tag envs K ("+" joins several: 4096+65536 10+50): tools/bench_fused.py sweep, steady window
   local O=gpurun_out/$1; mkdir -p $O
-  timeout -k 10 400 python tools/bench_fused.py --envs $2 --k $3 >> $O/fused.jsonl 2>> $O/fused.err || { tail -5 $O/fused.err; return 1; }
+  timeout -k 10 400 python tools/bench_fused.py --envs ${2//+/ } --k ${3//+/ } >> $O/fused.jsonl 2>> $O/fused.err || { tail -5 $O/fused.err; return 1; }
   cat $O/fused.jsonl
 }
 
