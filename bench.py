@@ -51,7 +51,9 @@ LAYOUT_WRITE = 176 + 16 + 104 + 1056 + 16 + 4 + 4 + 1 + 8  # bodies, scalars, sn
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node; > 1 without a launcher starts torch.distributed.run itself "
+                         "(default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
@@ -130,6 +132,15 @@ def cpu_baseline(args):
             "host": {"cpu_count": os.cpu_count(), "affinity": affinity, "cgroup_cpu_limit": quota, "model": model}}
 
 
+def launch_label(lane_group: int) -> str:
+    """config.launch: the step kernel's launch shape."""
+    if lane_group == 2:
+        return "lane pairs, 2 lanes per env (32 envs per wave, 2 waves per SIMD)"
+    if lane_group > 2:
+        return f"lane groups, {lane_group} lanes per env ({64 // lane_group} envs per wave)"
+    return "one lane per env, one wave per 64-env block"
+
+
 def regime(warmup: int, steps: int, max_steps: int) -> str:
     """Which part of the episode cycle the timed window covers (the cost of a step depends on
     it: DESIGN.md §7)."""
@@ -150,11 +161,12 @@ def regime_key(envs: int, max_steps: int, warmup: int, steps: int) -> str:
     return f"e{envs}_ms{max_steps}_w{warmup}_s{steps}"
 
 
-def load_pmc_traffic(key: str, kernel: str):
+def load_pmc_traffic(key: str, kernel: str, name: str = "pmc_step_kernel.json"):
     """The committed rocprofv3 PMC figures of the step kernel over the same timed window
     (dispatches warmup .. warmup + steps of a run with the same arguments), or None — also when
-    the profiled launch ran another kernel than this run's (lane groups or pairs)."""
-    path = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
+    the profiled launch ran another kernel than this run's (lane groups or pairs). `name`:
+    profiles/pmc_step_kernel.json (ms_step) or profiles/pmc_fused_kernel.json (ms_step_n)."""
+    path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as f:
             d = json.load(f)
@@ -166,12 +178,52 @@ def load_pmc_traffic(key: str, kernel: str):
         return None
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launcher_argv(gpus: int, argv: list, port: int) -> list:
+    """The command that runs this bench on `gpus` ranks of one node: torch.distributed.run with
+    one process per GPU (the driver's own form), the same bench arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def resolve_world(args, argv: list, env=None, run=None):
+    """--gpus N against the launcher's WORLD_SIZE. Returns the world size this process runs in, or
+    the exit code of a child launch: with N > 1 and no WORLD_SIZE (a plain `python bench.py --gpus
+    N`), torch.distributed.run starts N ranks of this script as a CHILD process (no exec: nothing
+    here has touched the GPU yet) and its return code is this process's; a launcher whose
+    WORLD_SIZE differs from an explicit --gpus is an error, so no N-GPU request can print a
+    one-GPU line."""
+    env = os.environ if env is None else env
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        if args.gpus is not None and args.gpus > 1:
+            import subprocess
+            run = run or subprocess.call
+            return {"exit": run(launcher_argv(args.gpus, argv, free_port()))}
+        if args.gpus is not None and args.gpus < 1:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} must be >= 1")
+        return {"world": 1}
+    world = int(ws)
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    return {"world": world}
+
+
 def main():
     args = parse()
+    how = resolve_world(args, sys.argv[1:])
+    if "exit" in how:
+        sys.exit(how["exit"])
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = how["world"]
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # MS_BENCH_SHARED_GPU=1 (rehearsal on a one-GPU box only): every rank on cuda:0, gloo for
@@ -268,10 +320,14 @@ def main():
     # the arbiter-cache entries the timed launches read and wrote (counted by the kernel)
     stats = batch.stats()
 
+    ranks_seen = 1
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if shared else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+        one = torch.ones(1, dtype=torch.int64, device="cpu" if shared else dev)
+        dist.all_reduce(one)  # every rank that took part in the timed window
+        ranks_seen = int(one.item())
 
     # With N > 1 ranks and no --allgather: a second, shorter timed loop WITH the whole-batch
     # obs all-gather after every step (BASELINE configs[3]; SURVEY.md 8(e) asks for the rate
@@ -311,73 +367,94 @@ def main():
     # as `value` (the reference's API hands back a contiguous stacked obs).
     ring_report = None
     if world == 1 and not ring and not args.no_ring_leg:
-        rb = FrameRingBatch(E, ring=32, config=cfg, device=dev.index)
+        R = 32
+        rb = FrameRingBatch(E, ring=R, config=cfg, device=dev.index)
         rb.reset(seed=19)
         rl = rb.launcher(actions, rb.rew, rb.term, rb.trunc, rb.goal, rb.score)
         for i in range(args.warmup):
             rl(i)
         torch.cuda.synchronize()
+        rb.reset_stats()
+        re0, re1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         r0 = time.perf_counter()
+        re0.record(rb.stream)
         for i in range(args.steps):
             rl(args.warmup + i)
+        re1.record(rb.stream)
         torch.cuda.synchronize()
         r_el = time.perf_counter() - r0
+        r_kern = re0.elapsed_time(re1) / args.steps
+        rst = rb.stats()
         rb.close()
+        r_arb = 0.5 * (rst["cache_entries_read"] + rst["cache_entries_written"]) / max(1, rst["env_steps"])
+        r_bytes = RING_BYTES + 2 * 352 / (R - 2) + 2 * ARB_BYTES * r_arb
+        r_ach = r_bytes * E / (r_kern * 1e-3) / 1e9
         ring_report = {"value": E * args.steps / r_el, "unit": "env-steps/s", "ms_per_step": r_el * 1e3 / args.steps,
-                       "R": 32, "kernel": "ms_step_ring_kernel",
-                       "obs": "strided (N, 4, 66) window into a (N, 4, 32, 22) frame ring, same values as obs "
-                              "(bench.py --frame-ring 32 gives its roofline line)"}
+                       "R": R, "kernel": "ms_step_ring_kernel",
+                       "roofline": {"bound": "hbm", "achieved": r_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": r_ach / HBM_PEAK_GBS, "traffic": None,
+                                    "kernel_ms": r_kern, "alg_bytes_per_env_step": r_bytes,
+                                    "alg_bytes_source": "SURVEY.md §8(d) without the prior frames' read and re-write: "
+                                                        f"881 + 2 x 352 B / (R - 2) wrap frames (R = {R}) + 2 x 20 B x "
+                                                        "mean cached arbiters (counted by the timed launches)"},
+                       "obs": f"strided (N, 4, 66) window into a (N, 4, {R}, 22) frame ring, same values as obs"}
 
-    # ms_step_n timed beside the headline (N = 1, default run): the same workload with the actions of
-    # K steps handed over per call (an open-loop rollout); with the lane-pair kernel one launch runs
-    # the K steps, each wave stepping its envs back to back. Same envs, seeds and window; its own
-    # pool of uniform actions (one (E, 4, 3) set per step, read from HBM) and its own (K, E, ...)
-    # outputs. Reported as `fused_steps`, never as `value` (the reference's API is one step per call).
+    # ms_step_n timed beside the headline (N = 1): the same workload with the actions of K steps handed
+    # over per call (an open-loop rollout); with the lane-pair kernel one launch runs the K steps, each
+    # wave stepping its envs back to back. Same envs and seeds, its own window (the headline's warm-up
+    # and timed steps rounded up to whole K-step launches, at least one warm-up and four timed
+    # launches, so that any --steps / --warmup emits it), its own pool of uniform actions (one
+    # (E, 4, 3) set per step, read from HBM) and its own (K, E, ...) outputs. Reported as
+    # `fused_steps`, never as `value` (the reference's API is one step per call).
     fused_report = None
     K = args.fused
-    if world == 1 and not ring and K > 0 and args.steps % K == 0 and args.warmup % K == 0:
+    if world == 1 and not ring and K > 0:
+        f_warm = K * max(1, -(-args.warmup // K))
+        f_steps = K * max(4, -(-args.steps // K))
         fb = SoccerBatch(E, config=cfg, device=dev.index)
         if args.lane_group is not None:
             fb.set_lane_group(args.lane_group)
         fb.reset(seed=19)
-        fsets = max(1, min(args.steps // K, int(args.action_gib * (1 << 30) // (E * 48 * K))))
+        fsets = max(1, min(f_steps // K, int(args.action_gib * (1 << 30) // (E * 48 * K))))
         fpool = [torch.rand((K, E, 4, 3), device=dev, generator=gen) * 2 - 1 for _ in range(fsets)]
         fout = {name: torch.empty((K, E) + sh, dtype=dt, device=dev) for name, dt, sh in
                 (("obs", torch.float32, (4, 66)), ("rew", torch.float32, (4,)), ("term", torch.uint8, (4,)),
                  ("trunc", torch.uint8, (4,)), ("goal", torch.int8, ()), ("score", torch.int32, (2,)))}
-        for i in range(args.warmup // K):
+        for i in range(f_warm // K):
             fb.step_n(fpool[i % fsets], out=fout)
         torch.cuda.synchronize()
         fb.reset_stats()
         fe0, fe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         f0 = time.perf_counter()
         fe0.record(fb.stream)
-        for i in range(args.steps // K):
+        for i in range(f_steps // K):
             fb.step_n(fpool[i % fsets], out=fout)
         fe1.record(fb.stream)
         torch.cuda.synchronize()
         f_el = time.perf_counter() - f0
-        f_kern = fe0.elapsed_time(fe1) / args.steps
+        f_kern = fe0.elapsed_time(fe1) / f_steps
         fk = {"ms_step_pair_kernel": "ms_step_pair_n_kernel", "ms_step_group_kernel": "ms_step_group_n_kernel"}.get(
             fb.step_kernel, fb.step_kernel)
         fst = fb.stats()
         f_arb = 0.5 * (fst["cache_entries_read"] + fst["cache_entries_written"]) / max(1, fst["env_steps"])
         f_bytes = SURVEY_BYTES + 2 * ARB_BYTES * f_arb
         f_ach = f_bytes * E / (f_kern * 1e-3) / 1e9
-        # HBM bytes per env-step of the committed rocprofv3 PMC passes over this kernel (same E, K)
-        f_traffic, f_src = None, None
-        pf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04k", "pmc_fused.json")
-        if os.path.exists(pf):
-            pm = json.load(open(pf))
-            if pm.get("envs") == E and pm.get("K") == K and pm.get("kernel", "").startswith(fk):
-                f_traffic = pm["hbm_bytes_per_env_step"] * E / (f_kern * 1e-3) / 1e9
-                f_src = "profiles/r04k/pmc_fused.json (FETCH_SIZE x 2 + WRITE_SIZE per env-step) over this run's time"
-        fused_report = {"value": E * args.steps / f_el, "unit": "env-steps/s", "K": K,
-                        "ms_per_step": f_el * 1e3 / args.steps, "kernel": fk, "kernel_ms_per_step": f_kern,
-                        "launches": args.steps // K if fb.lane_group > 0 else args.steps,
+        # HBM bytes per env-step of the committed rocprofv3 PMC passes over this kernel and window
+        fkey = f"e{E}_ms{args.max_steps}_K{K}_w{f_warm}_s{f_steps}"
+        fpm = load_pmc_traffic(fkey, fk, "pmc_fused_kernel.json")
+        f_traffic = None if fpm is None else fpm["hbm_bytes_per_launch"] / K / (f_kern * 1e-3) / 1e9
+        fused_report = {"value": E * f_steps / f_el, "unit": "env-steps/s", "K": K, "warmup": f_warm,
+                        "steps": f_steps, "ms_per_step": f_el * 1e3 / f_steps, "kernel": fk,
+                        "kernel_ms_per_step": f_kern,
+                        "launches": f_steps // K if fb.lane_group > 0 else f_steps,
+                        "regime": regime(f_warm, f_steps, args.max_steps),
                         "roofline": {"bound": "hbm", "achieved": f_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                     "frac": f_ach / HBM_PEAK_GBS, "traffic": f_traffic, "traffic_source": f_src,
-                                     "alg_bytes_per_env_step": f_bytes},
+                                     "frac": f_ach / HBM_PEAK_GBS, "traffic": f_traffic,
+                                     "frac_measured": None if f_traffic is None else f_traffic / HBM_PEAK_GBS,
+                                     "traffic_source": (f"{fpm['source']} window {fkey} (rocprofv3 FETCH_SIZE x 2 + "
+                                                        "WRITE_SIZE per launch / K) over this run's kernel time")
+                                                       if fpm else f"no committed PMC pass of {fk} for window {fkey}",
+                                     "kernel_ms": f_kern, "alg_bytes_per_env_step": f_bytes},
                         "arbiter_overflow": fst["arbiter_overflow"],
                         "actions": f"{fsets} distinct (K, E, 4, 3) uniform(-1,1) blocks",
                         "api": "SoccerBatch.step_n / ms_step_n: K steps with the actions given up front (open loop)"}
@@ -419,6 +496,7 @@ def main():
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
@@ -436,8 +514,7 @@ def main():
                                     else ""),
                        "envs_per_gpu": E, "global_envs": world * E, "max_steps": args.max_steps,
                        "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else ""),
-                       "launch": (f"lane groups, {batch.lane_group} lanes per env ({64 // batch.lane_group} envs "
-                                  "per wave)" if not ring and batch.lane_group > 0 else "one wave per 64-env block"),
+                       "launch": launch_label(batch.lane_group if not ring else 0),
                        **({"obs_layout": f"frame ring, R = {ring} (opt-in; obs is a strided (N, 4, 66) window)"}
                           if ring else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 4
+#define MS_ABI_VERSION 5
 
 #define MS_N_AGENTS 4
 #define MS_N_BODIES 5 /* 4 agents + ball */
@@ -173,7 +173,7 @@ typedef struct ms_stats {
   uint64_t arbiter_overflow;  /* arbiters dropped because MS_MAX_ARBITERS was full */
   uint64_t nonfinite_envs;    /* env-steps skipped because an action was not finite */
   int64_t first_nonfinite_env;/* lowest env index with a non-finite action, -1 if none */
-  /* Since the last ms_reset_stats, counted inside ms_step / ms_step_ring (ABI 2): env-steps
+  /* Since the last ms_reset_stats, counted inside ms_step, ms_step_n and ms_step_ring (ABI 2): env-steps
    * taken, and the arbiter-cache entries they read (the previous step's cache) and wrote (this
    * step's), i.e. the warm-start cache traffic of the algorithmic byte count (20 B per entry).
    * Kept as 64-bit counts per 64-env block on the device: they do not wrap within a run. */
@@ -219,8 +219,10 @@ int ms_reset(ms_env *env, const uint64_t *pcg, const uint8_t *env_mask, int mode
 
 /* One env.step for every env (see layouts above). obs must be non-NULL; rew, term,
  * trunc, goal, score may be NULL (not written). An env whose actions contain a
- * non-finite value is not stepped and its outputs are not written; it is counted in
- * ms_stats (read with ms_get_stats, which synchronises). */
+ * non-finite value is not stepped (SoccerEnv.step raises ValueError there, soccer_env.py:116-117);
+ * it is counted in ms_stats (read with ms_get_stats, which synchronises) and its outputs get
+ * defined values (ABI 5): obs all NaN, rew (NaN, NaN, 0, 0), term / trunc / goal 0, score the
+ * env's current score. */
 int ms_step(ms_env *env, const float *actions, float *obs, float *rew, uint8_t *term,
             uint8_t *trunc, int8_t *goal, int32_t *score);
 
@@ -233,9 +235,9 @@ int ms_step(ms_env *env, const float *actions, float *obs, float *rew, uint8_t *
  * each wave stepping its envs K times back to back (a wave slowed by a pile-up in one step no
  * longer holds the whole grid at every step boundary); the one-lane-per-env kernel (lanes 0)
  * issues K ms_step launches. An env whose actions at step k are not all finite is skipped for
- * that step exactly as ms_step skips it: counted in ms_stats, its step-k reward NaN, and its other
- * step-k outputs not written (ms_step's batch buffer keeps the previous values; here the caller's
- * K-step slot keeps what it held).
+ * that step exactly as ms_step skips it: counted in ms_stats, and its step-k outputs take
+ * ms_step's defined values for a skipped env-step (NaN obs and rewards, term / trunc / goal 0, the
+ * current score).
  * 1 <= K, alignment as ms_step; MS_ERR_INVALID_ARGUMENT otherwise. */
 int ms_step_n(ms_env *env, int K, const float *actions, float *obs, float *rew, uint8_t *term,
               uint8_t *trunc, int8_t *goal, int32_t *score);
@@ -261,7 +263,8 @@ int ms_set_group_solve(ms_env *env, int mode);
 int ms_get_group_solve(const ms_env *env);
 
 /* Name of the kernel the next ms_step launches for this handle's batch size and launch shape
- * ("ms_step_kernel", "ms_step_pipe_kernel", "ms_step_group_kernel", ...), as rocprofv3 lists it
+ * ("ms_step_kernel", "ms_step_group_kernel" or "ms_step_pair_kernel"; ms_step_n runs the
+ * matching "_n" kernel), as rocprofv3 lists it
  * (without template arguments): what bench.py's roofline line and its PMC lookup are keyed on.
  * Host-only; "" for a null handle. */
 const char *ms_step_kernel_name(const ms_env *env);

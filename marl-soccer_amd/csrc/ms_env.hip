@@ -1290,6 +1290,29 @@ __device__ __forceinline__ void unpack_scalars(int4 v, Env& E) {
   E.rng.u32 = (uint32_t)v.w;
 }
 __device__ __forceinline__ void load_scalars(At a, Env& E) { unpack_scalars(*plane<int4>(a, OFF_I4, 0), E); }
+
+// The outputs of an env-step skipped for a non-finite action (SoccerEnv.step raises ValueError there,
+// soccer_env.py:116-117, and the env is not stepped): defined values, so that a caller who does not
+// look at the NaN reward reads no stale or uninitialised episode end (a ms_step_n output slot would
+// otherwise keep whatever it held). Reward (NaN, NaN, 0, 0), term / trunc / goal 0, the env's current
+// score (sc: its scalars group), the stacked observation all NaN. `part` of `parts` cooperating lanes
+// writes every parts-th 16-B piece of the 1,056-B obs row; lane part 0 writes the rest.
+__device__ __forceinline__ void skipped_outputs(int64_t e, int4 sc, int part, int parts, float* __restrict__ obs,
+                                                float* __restrict__ rew, uint8_t* __restrict__ term,
+                                                uint8_t* __restrict__ trunc, int8_t* __restrict__ goal_out,
+                                                int32_t* __restrict__ score_out) {
+  const float qn = __builtin_nanf("");
+  if (obs) {
+    float4* row = (float4*)(obs + e * 264);
+    for (int q = part; q < 66; q += parts) row[q] = make_float4(qn, qn, qn, qn);
+  }
+  if (part != 0) return;
+  if (rew) *(float4*)(rew + e * 4) = make_float4(qn, qn, 0.0f, 0.0f);
+  if (term) *(uint32_t*)(term + e * 4) = 0u;
+  if (trunc) *(uint32_t*)(trunc + e * 4) = 0u;
+  if (goal_out) goal_out[e] = 0;
+  if (score_out) *(int2*)(score_out + e * 2) = make_int2((int)((uint32_t)sc.y & 0xffffu), (int)((uint32_t)sc.y >> 16));
+}
 __device__ __forceinline__ void store_scalars(At a, const Env& E) {
   *plane<int4>(a, OFF_I4, 0) = make_int4(E.steps, (int32_t)(((uint32_t)E.score_blue & 0xffffu) | ((uint32_t)E.score_red << 16)),
                       (int32_t)E.meta, (int32_t)E.rng.u32);
@@ -1429,8 +1452,9 @@ __device__ __forceinline__ void step_block(const DevState& S, const Params& P, L
       atomicAdd(&ctr->nonfinite, 1ULL);
       atomicMin(&ctr->first_bad, (long long)e);
       // the env is not stepped; its reward is poisoned so that no caller reads the previous
-      // step's value as this one's (the reference raises ValueError here)
-      if (rew) *(float4*)(rew + e * 4) = make_float4(__builtin_nanf(""), __builtin_nanf(""), 0.0f, 0.0f);
+      // step's value as this one's (the reference raises ValueError here), and its other outputs
+      // get defined values (skipped_outputs; the frame ring writes no frame: FrameRingBatch)
+      skipped_outputs(e, F.sc, 0, 1, RING ? nullptr : obs, rew, term, trunc, goal_out, score_out);
       active = false;
     }
   }

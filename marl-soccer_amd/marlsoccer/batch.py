@@ -179,8 +179,9 @@ class SoccerBatch:
     def step(self, actions: torch.Tensor, check: bool = False) -> StepOutput:
         """One env.step for all envs; actions (N, 4, 3) float32 on the env's device.
 
-        An env whose actions are not all finite is not stepped: its reward comes back NaN and
-        the library counts it (ms_get_stats). check=True synchronises and raises the
+        An env whose actions are not all finite is not stepped: its reward and observation come
+        back NaN, its term / trunc / goal 0 and its score unchanged (defined values, so no stale
+        episode end is read), and the library counts it (ms_get_stats). check=True synchronises and raises the
         reference's ValueError (soccer_env.py:116-117) for the first such env; otherwise call
         raise_if_nonfinite() at a point that synchronises anyway (DeviceRollout does, once
         per rollout)."""
@@ -211,13 +212,16 @@ class SoccerBatch:
             self.raise_if_nonfinite(actions)
         return StepOutput((self.obs, self.rew, self.term, self.trunc, self.goal, self.score))
 
-    def step_n(self, actions: torch.Tensor, out: dict | None = None) -> StepOutput:
+    def step_n(self, actions: torch.Tensor, out: dict | None = None, check: bool = False) -> StepOutput:
         """K consecutive steps with the actions given up front (ms_step_n): actions (K, N, 4, 3)
         float32 on the env's device, e.g. a random-action rollout. Returns the K steps' outputs
         with a leading K dimension (obs (K, N, 4, 66), rew (K, N, 4), term / trunc (K, N, 4),
         goal (K, N), score (K, N, 2)); `out` may hold any of those tensors to write into. Bit for
         bit what K step() calls return; with the lane-pair and lane-group kernels (the defaults) the K
-        steps are one launch."""
+        steps are one launch. An env-step skipped for a non-finite action writes step()'s defined
+        values into its slot (NaN obs and rewards, term / trunc / goal 0, the current score);
+        check=True synchronises and raises the reference's ValueError for the first such env, as
+        step(check=True) does."""
         if actions.dim() != 4 or actions.shape[1:] != (self.num_envs, 4, 3):
             raise ValueError(f"actions must have shape (K, {self.num_envs}, 4, 3), got {tuple(actions.shape)}")
         K = int(actions.shape[0])
@@ -243,6 +247,12 @@ class SoccerBatch:
                                    self._ptr(o["score"]))
             self._leave(cur, actions)
         N.check(rc, "ms_step_n")
+        if check:
+            st = self.stats()
+            if st["nonfinite_envs"]:
+                e = st["first_nonfinite_env"]
+                bad = (~torch.isfinite(actions[:, e]).all(dim=-1)).any(dim=-1).nonzero()
+                self.raise_if_nonfinite(actions[int(bad[0, 0])] if bad.numel() else None)
         return StepOutput((o["obs"], o["rew"], o["term"], o["trunc"], o["goal"], o["score"]))
 
     def raise_if_nonfinite(self, actions: torch.Tensor | None = None) -> None:
@@ -382,7 +392,12 @@ class SoccerBatch:
 
     @property
     def step_kernel(self) -> str:
-        """Name of the kernel the next step launches (ms_step_kernel_name), as rocprofv3 lists it."""
+        """Name of the kernel the next step launches (ms_step_kernel_name), as rocprofv3 lists it.
+        A library without that symbol (an older build timed by tools/variants.py) is named from
+        its lane group instead."""
+        if not hasattr(self._L, "ms_step_kernel_name"):
+            g = self.lane_group
+            return "ms_step_pair_kernel" if g == 2 else ("ms_step_group_kernel" if g > 2 else "ms_step_kernel")
         return self._L.ms_step_kernel_name(self._h).decode()
 
     def synchronize(self) -> None:

@@ -45,3 +45,12 @@ def test_bench_prints_one_contract_line():
     cache = rl["cache_entries_per_env_step"]
     assert cache["env_steps_counted"] == 4096 * 30 and cache["read"] >= 0 and cache["written"] >= 0
     assert abs(rl["mean_cached_arbiters"] - 0.5 * (cache["read"] + cache["written"])) < 1e-9
+    assert d["ranks_seen"] == 1 and d["config"]["launch"].startswith("lane groups, 8 lanes per env")
+    # the K-step leg is in the line at the driver's short window too (its own whole-launch window)
+    fs = d["fused_steps"]
+    assert fs["K"] == 50 and fs["warmup"] == 50 and fs["steps"] == 200 and fs["value"] > 0
+    assert fs["roofline"]["bound"] == "hbm" and 0 < fs["roofline"]["frac"] < 1
+    assert abs(fs["roofline"]["frac"] - fs["roofline"]["achieved"] / fs["roofline"]["peak"]) < 1e-9
+    # and the frame-ring leg carries its own roofline block
+    fr = d["frame_ring"]
+    assert fr["R"] == 32 and fr["value"] > 0 and 0 < fr["roofline"]["frac"] < 1

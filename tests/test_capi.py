@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_config_defaults():
     from marlsoccer import _native as N
-    assert N.lib().ms_abi_version() == 4
+    assert N.lib().ms_abi_version() == 5
     c = N.default_config()
     assert c.max_velocity == 200 and c.agent_mass == 10 and c.ball_mass == 1
     assert c.action_force_max == 150000.0 and c.action_torque_max == 1000.0 and c.max_steps == 1000

@@ -235,6 +235,11 @@ def test_nonfinite_actions_skip_env_and_count(ms, lanes):
     assert (st["steps"][[5, 9]] == 0).all() and (np.delete(st["steps"], [5, 9]) == 1).all()
     rew = gpu.rew.cpu().numpy()
     assert np.isnan(rew[[5, 9], :2]).all() and np.isfinite(np.delete(rew, [5, 9], axis=0)).all()
+    # the skipped envs' other outputs are defined (ABI 5): NaN obs, no episode end, no goal, score kept
+    obs = gpu.obs.cpu().numpy()
+    assert np.isnan(obs[[5, 9]]).all() and np.isfinite(np.delete(obs, [5, 9], axis=0)).all()
+    assert (gpu.term.cpu().numpy()[[5, 9]] == 0).all() and (gpu.trunc.cpu().numpy()[[5, 9]] == 0).all()
+    assert (gpu.goal.cpu().numpy()[[5, 9]] == 0).all() and (gpu.score.cpu().numpy()[[5, 9]] == 0).all()
     # the device path raises the reference's ValueError (soccer_env.py:116-117) when asked
     with pytest.raises(ValueError, match=r"Action contains non-finite values for agent 'agent_2'"):
         gpu.raise_if_nonfinite(act)

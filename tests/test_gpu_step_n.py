@@ -149,22 +149,38 @@ def test_step_n_nonfinite_actions_skip_like_step(ms, lanes):
     acts[3, 5, 1, 0] = float("nan")
     acts[3, 200, 3, 2] = float("inf")
     acts[7, 5, 0, 1] = float("-inf")
-    res = b.step_n(acts)
+    # a slot full of garbage: a skipped env-step must overwrite it with defined values (ABI 5)
+    out = {"obs": torch.full((K, n, 4, 66), 7.0, device=a.device),
+           "term": torch.full((K, n, 4), 1, dtype=torch.uint8, device=a.device),
+           "trunc": torch.full((K, n, 4), 1, dtype=torch.uint8, device=a.device),
+           "goal": torch.full((K, n), 3, dtype=torch.int8, device=a.device),
+           "score": torch.full((K, n, 2), -5, dtype=torch.int32, device=a.device)}
+    res = b.step_n(acts, out=out)
     skipped = {(3, 5), (3, 200), (7, 5)}
     for k in range(K):
+        score_before = a.score.clone()
         o = a.step(acts[k])
-        # a skipped env-step writes only its NaN reward (ms_step_n's contract, as ms_step's: the
-        # per-step batch buffer keeps the env's previous outputs, a K-step output slot keeps what
-        # it held): compare every other env
-        keep = torch.tensor([(k, e) not in skipped for e in range(n)], device=a.device)
-        for f in ("obs", "term", "trunc", "goal", "score"):
-            assert torch.equal(getattr(o, f)[keep], getattr(res, f)[k][keep]), f"{f} step {k}"
-        # rewards bit for bit, NaN included
-        assert torch.equal(o.rew.view(torch.int32), res.rew[k].view(torch.int32)), f"rew step {k}"
+        # every env bit for bit, the skipped ones included (NaN obs and rewards, term / trunc / goal
+        # 0, the score unchanged: ms_step's and ms_step_n's defined values)
+        for f in ("obs", "rew"):
+            x, y = getattr(o, f), getattr(res, f)[k]
+            assert torch.equal(x.view(torch.int32), y.view(torch.int32)), f"{f} step {k}"
+        for f in ("term", "trunc", "goal", "score"):
+            assert torch.equal(getattr(o, f), getattr(res, f)[k]), f"{f} step {k}"
+        for (ks, e) in skipped:
+            if ks != k:
+                continue
+            assert torch.isnan(res.obs[k, e]).all() and torch.isnan(res.rew[k, e, :2]).all()
+            assert (res.term[k, e] == 0).all() and (res.trunc[k, e] == 0).all() and int(res.goal[k, e]) == 0
+            assert torch.equal(res.score[k, e], score_before[e])
     assert torch.isnan(res.rew[3, 5]).any() and torch.isnan(res.rew[3, 200]).any() and torch.isnan(res.rew[7, 5]).any()
     assert not torch.isnan(res.rew[4]).any()
     assert_state_equal(b.export_state(), a.export_state(), "end")
     sa, sb = a.stats(), b.stats()
     assert sa["nonfinite_envs"] == sb["nonfinite_envs"] == 3
+    # step_n(check=True) raises the reference's ValueError for the first such env (and clears the count)
+    with pytest.raises(ValueError, match=r"non-finite values for agent 'agent_1'.*env 5"):
+        b.step_n(acts[:4], check=True)
+    b.step_n(acts[4:6], check=True)
     a.close()
     b.close()

@@ -13,7 +13,8 @@
 #   tools/gpu.sh fused    <tag> <envs> <K>       K-step launch sweep (tools/bench_fused.py; "+" joins values)
 #   tools/gpu.sh pmcfused <tag> <envs> <K>      FETCH/WRITE PMC passes + kernel trace over the K-step launch
 #   tools/gpu.sh stamps   <tag> [G=lanes] <envs...>  per-phase wave stamps (tools/stamps.py; stamps library prebuilt)
-#   tools/gpu.sh rehearse <tag>                 bench.py --gpus 2 with both ranks on cuda:0 (gloo), 2 x 8,192 and 2 x 65,536
+#   tools/gpu.sh rehearse <tag>                 plain `bench.py --gpus 2` (it starts torchrun itself), both ranks on cuda:0 (gloo)
+#   tools/gpu.sh driver   <tag>                 the driver's own `bench.py --gpus 1 --steps 20 --warmup 5` line
 #   tools/gpu.sh policy   <tag>                 policy/rollout GPU tests + bench_policy + graph rollouts
 #
 # Several jobs in one call: tools/gpu.sh multi "suite r04a" "sq r04a_sq 65536" ...
@@ -74,7 +75,7 @@ profile() {
   for WS in "5 20" "1000 1000"; do
     read W S <<< "$WS"
     for C in FETCH_SIZE WRITE_SIZE; do
-      timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_${C}_w${W}_s${S} -o run -- python bench.py --warmup $W --steps $S --no-cpu-baseline --no-ring-leg --fused 0 "$@" > $O/pmc_${C}_w${W}_s${S}.log 2>&1 \
+      timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_${C}_w${W}_s${S} -o run -- python bench.py --warmup $W --steps $S --no-cpu-baseline --no-ring-leg "$@" > $O/pmc_${C}_w${W}_s${S}.log 2>&1 \
         || { echo "pmc $C w$W s$S failed"; tail -20 $O/pmc_${C}_w${W}_s${S}.log; return 1; }
     done
   done
@@ -140,15 +141,21 @@ stamps() {  # tag [G=lanes] envs...
   done
 }
 
-rehearse() {
+rehearse() {  # bench.py --gpus 2 through the PLAIN entry (bench.py starts torch.distributed.run itself), both ranks on cuda:0 (gloo)
   local O=gpurun_out/$1; mkdir -p $O
   local E
   for E in 8192 65536; do
-    MS_BENCH_SHARED_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-      --master-port 29517 bench.py --gpus 2 --envs $E --steps 200 --warmup 50 > $O/bench_shared2_e$E.json 2> $O/bench_shared2_e$E.err \
+    MS_BENCH_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 2 --envs $E --steps 200 --warmup 50 > $O/bench_shared2_e$E.json 2> $O/bench_shared2_e$E.err \
       || { echo "shared bench E=$E failed"; tail -20 $O/bench_shared2_e$E.err; return 1; }
     cat $O/bench_shared2_e$E.json
   done
+}
+
+driver() {  # the driver's own bench command, N = 1 (BENCH_rNN.json)
+  local O=gpurun_out/$1; mkdir -p $O
+  timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err \
+    || { echo "driver bench failed"; tail -20 $O/bench_driver.err; return 1; }
+  cat $O/bench_driver.json
 }
 
 policy() {

@@ -41,17 +41,22 @@ def compiler_usage(tag, kernel):
     return dict(out, source=f"profiles/{tag}_resource_usage.txt", kernel=f"{kernel}<true> (default physics)") if out else None
 
 
-def window_pmc(src, kernel, envs, warmup, steps):
-    """HBM bytes per launch over dispatches [warmup, warmup + steps) of the step kernel in the
-    FETCH_SIZE and WRITE_SIZE passes of one bench window (medians over the window)."""
+def window_pmc(src, kernel, envs, warmup, steps, pass_w=None, pass_s=None, per_launch_steps=1):
+    """HBM bytes per launch over dispatches [warmup, warmup + steps) of `kernel` in the
+    FETCH_SIZE and WRITE_SIZE passes of one bench window (medians over the window). pass_w /
+    pass_s name the bench pass when the kernel's own window differs from it (the K-step leg);
+    hbm_bytes_per_env_step divides by envs x per_launch_steps."""
     out = {}
     vals = {}
+    pw, ps = (warmup if pass_w is None else pass_w), (steps if pass_s is None else pass_s)
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        path = os.path.join(src, f"pmc_{c}_w{warmup}_s{steps}", "run_counter_collection.csv")
+        path = os.path.join(src, f"pmc_{c}_w{pw}_s{ps}", "run_counter_collection.csv")
         if not os.path.exists(path):
             return None
         _, rows = per_kernel(path, kernel)
         rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        if not rows:
+            return None
         win = rows[warmup:warmup + steps]
         vals[c] = [float(r["Counter_Value"]) for r in win]
         out["dispatches"] = [warmup, warmup + len(win)]
@@ -65,7 +70,27 @@ def window_pmc(src, kernel, envs, warmup, steps):
     rd, wr = 2.0 * fetch_kib * 1024, write_kib * 1024
     out.update({"FETCH_SIZE_KiB_median": fetch_kib, "WRITE_SIZE_KiB_median": write_kib,
                 "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
-                "hbm_bytes_per_env_step": (rd + wr) / envs})
+                "hbm_bytes_per_env_step": (rd + wr) / (envs * per_launch_steps)})
+    return out
+
+
+def fused_summary(tag, src, dst, envs, kernel, K, max_steps):
+    """profiles/pmc_fused_kernel.json: the K-step leg's (bench.py `fused_steps`) launches in the same
+    PMC passes: its own window is the pass's warm-up and steps rounded up to whole K-step launches
+    (at least one warm-up and four timed launches), as bench.py computes it."""
+    nk = kernel.replace("_kernel", "_n_kernel")
+    out = {"tag": tag, "kernel": nk, "envs": envs, "K": K,
+           "correction": "read = 2 x FETCH_SIZE (gfx950 half-count, MI355X_MICROARCH.md HBM); write = WRITE_SIZE",
+           "regimes": {}}
+    for w, s in ((5, 20), (1000, 1000)):
+        fw, fs = K * max(1, -(-w // K)), K * max(4, -(-s // K))
+        r = window_pmc(src, nk, envs, fw // K, fs // K, pass_w=w, pass_s=s, per_launch_steps=K)
+        if r is not None:
+            out["regimes"][f"e{envs}_ms{max_steps}_K{K}_w{fw}_s{fs}"] = r
+    if out["regimes"]:
+        with open(os.path.join(dst, "pmc_fused_kernel.json"), "w") as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps(out, indent=1))
     return out
 
 
@@ -101,6 +126,7 @@ def main(tag, envs=65536, kernel="ms_step_kernel", warmup=1000, steps=1000, max_
         with open(os.path.join(dst, name), "w") as f:
             json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
+    fused_summary(tag, src, dst, envs, kernel, 50, max_steps)
 
 
 if __name__ == "__main__":

@@ -16,7 +16,7 @@ import json
 import statistics
 from collections import defaultdict
 
-STEP = ("ms_step_kernel", "ms_step_pipe_kernel", "ms_step_group_kernel", "ms_step_pair_kernel",
+STEP = ("ms_step_kernel", "ms_step_group_kernel", "ms_step_pair_kernel",
         "ms_step_pair_n_kernel", "ms_step_group_n_kernel")
 
 
