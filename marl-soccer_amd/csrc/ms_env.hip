@@ -106,12 +106,17 @@ struct Counters {
 
 
 #ifdef MS_STAMPS
+// slot k: s_memtime (shader cycles; its counter is per XCD, so cross-wave comparisons hold within
+// an XCD only); slot 24 + k: s_memrealtime (the 100-MHz clock every XCD shares: the launch timeline)
 #define STAMP(k)                                                                         \
   do {                                                                                   \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
+    unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                            \
     const unsigned long long act_ = __ballot(1);                                          \
-    if ((int)(threadIdx.x & 63) == __ffsll((long long)act_) - 1 && S.stamps)              \
-      S.stamps[stamp_row * MS_NSTAMP + (k)] = t_;                                               \
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)act_) - 1 && S.stamps) {            \
+      S.stamps[stamp_row * MS_NSTAMP + (k)] = t_;                                        \
+      S.stamps[stamp_row * MS_NSTAMP + 24 + (k)] = r_;                                   \
+    }                                                                                    \
   } while (0)
 // cycles spent inside a region of a divergent loop, accumulated per lane; the wave's figure is
 // the maximum over its lanes (the lane that ran the most iterations), written to slot k
@@ -136,7 +141,7 @@ struct Counters {
 #define ACC_INC(v) do { } while (0)
 #define ACC_STORE(v, k) do { } while (0)
 #endif
-#define MS_NSTAMP 24
+#define MS_NSTAMP 48  // [0, 24): cycles and accumulators; [24, 48): real time of stamps 0..23
 
 // ---- per-lane env register file ------------------------------------------------------------
 struct Env {
@@ -2087,7 +2092,7 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
   if (((uintptr_t)actions & 15u) || ((uintptr_t)obs & 7u) || ((uintptr_t)rew & 15u) || ((uintptr_t)term & 3u) ||
       ((uintptr_t)trunc & 3u) || ((uintptr_t)score & 7u))
     return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: misaligned buffer (actions/rew 16 B, obs/score 8 B, flags 4 B)");
-  const unsigned nblk = grid_for(h->n, MS_BLOCK);
+  [[maybe_unused]] const unsigned nblk = grid_for(h->n, MS_BLOCK);
   if (h->group == 2) {
     const dim3 grid(grid_for(h->n, pr::EPW));
     if (h->default_params)
@@ -2096,7 +2101,11 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
     else
       hipLaunchKernelGGL(ms_step_pair_kernel<false>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew,
                          term, trunc, goal, score, h->ctr);
-  } else if (h->group > 0) {
+  } else {
+#ifdef MS_PAIR_ONLY  // experiment builds (tools/variants.py): the lane-pair kernels only
+    return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: this experiment build has the lane-pair kernel only");
+#else
+  if (h->group > 0) {
     const int G = h->group;
     const dim3 grid(grid_for(h->n, 64 / G));
     if (G == 8) {
@@ -2121,6 +2130,8 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
     hipLaunchKernelGGL(ms_step_kernel<false>, dim3(nblk), dim3(MS_BLOCK), 0, h->stream, h->S, h->P, actions, obs,
                        rew, term, trunc, goal, score, h->ctr);
   }
+#endif
+  }
   HIPCHK(hipGetLastError());
   return MS_OK;
 }
@@ -2144,6 +2155,7 @@ int ms_step_n(ms_env* h, int K, const float* actions, float* obs, float* rew, ui
     HIPCHK(hipGetLastError());
     return MS_OK;
   }
+#ifndef MS_PAIR_ONLY
   if (h->group > 0) {
     const int G = h->group;
     const dim3 grid(grid_for(h->n, 64 / G));
@@ -2165,6 +2177,7 @@ int ms_step_n(ms_env* h, int K, const float* actions, float* obs, float* rew, ui
     HIPCHK(hipGetLastError());
     return MS_OK;
   }
+#endif
   const int64_t n = h->n;
   for (int k = 0; k < K; ++k) {
     const int64_t o = (int64_t)k * n;
@@ -2233,12 +2246,17 @@ int ms_step_ring(ms_env* h, const float* actions, float* frames, int R, int pos,
       ((uintptr_t)score & 7u))
     return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_ring: misaligned buffer (actions/rew 16 B, score 8 B, flags 4 B)");
   const Ring rg{frames, R, pos, wrap};
+#ifdef MS_PAIR_ONLY
+  (void)rg;
+  return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_ring: this experiment build has the lane-pair kernel only");
+#else
   if (h->default_params)
     hipLaunchKernelGGL(ms_step_ring_kernel<true>, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S,
                        h->P, actions, rg, rew, term, trunc, goal, score, h->ctr);
   else
     hipLaunchKernelGGL(ms_step_ring_kernel<false>, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S,
                        h->P, actions, rg, rew, term, trunc, goal, score, h->ctr);
+#endif
   HIPCHK(hipGetLastError());
   return MS_OK;
 }

@@ -151,6 +151,22 @@ rehearse() {  # bench.py --gpus 2 through the PLAIN entry (bench.py starts torch
   done
 }
 
+vrun() {  # tag name...: time lib/exp variants (tools/variants.py run), steady window then the driver's window, twice
+  local O=gpurun_out/$1; shift; mkdir -p $O
+  local r
+  for r in 1 2; do
+    timeout -k 10 600 python tools/variants.py run --envs 65536 "$@" >> $O/variants.txt 2>&1 || { tail -20 $O/variants.txt; return 1; }
+    timeout -k 10 600 python tools/variants.py run --envs 65536 --steps 20 --warmup 5 "$@" >> $O/variants_driver.txt 2>&1 || { tail -20 $O/variants_driver.txt; return 1; }
+  done
+  cat $O/variants.txt $O/variants_driver.txt
+}
+
+vstamps() {  # tag lib-name envs: per-phase stamps of a -DMS_STAMPS lib/exp variant
+  local O=gpurun_out/$1; mkdir -p $O
+  timeout -k 10 240 python tools/stamps.py --lib marl-soccer_amd/lib/exp/lib_$2.so --envs $3 --steps 300 --warmup 1000 --every 10 --out $O/stamps_$2_$3.json > $O/stamps_$2_$3.log 2>&1 || { tail $O/stamps_$2_$3.log; return 1; }
+  python -c "import json; d=json.load(open('$O/stamps_$2_$3.json')); print('$2', $3, 'mean', round(d['wave_cycles_mean']), 'slow5', round(d['wave_cycles_slowest5pct']), 'worst', round(d.get('worst_wave_cycles_mean', 0)), {k: round(v['mean']) for k, v in d['phases'].items()}); t=d['timeline']; print({k: v for k, v in t.items() if k != 'waves_in_phase_per_us_bin'})"
+}
+
 driver() {  # the driver's own bench command, N = 1 (BENCH_rNN.json)
   local O=gpurun_out/$1; mkdir -p $O
   timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err \

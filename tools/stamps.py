@@ -21,7 +21,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "marl-soccer_amd")
 STAMP_LIB = os.path.join(PKG, "lib", "libmarlsoccer_stamps.so")
-NS = 24  # MS_NSTAMP
+NS = 48  # MS_NSTAMP: [0, 24) s_memtime cycles and accumulators, [24, 48) s_memrealtime (100 MHz) of stamps 0..23
+RT = 24
 # accumulated narrowphase sub-phase cycles and iteration counts (wave max over lanes)
 ACC = {16: "AA test", 17: "AA insert", 18: "AA iterations", 19: "SA test", 20: "SA insert", 21: "SA iterations"}
 
@@ -31,6 +32,42 @@ LABELS = {1: "load+actions", 2: "integrate+transforms", 11: "bp+nphase AA/BA", 1
           3: "nphase ball-wall+cache age", 14: "prestep", 4: "velocity", 15: "warm start",
           22: "solver schedule (lane groups)", 5: "solver x10",
           6: "cache write", 7: "meta", 8: "goal+reward+outputs", 9: "obs frames+snap", 10: "state stores"}
+
+
+def timeline(st):
+    """One launch on the shared 100-MHz clock: when waves start and end, and how many waves are in
+    the load, physics (narrowphase .. solver), and output (goal .. state stores) phases per 1-us bin."""
+    import numpy as np
+    rt = st[:, RT:RT + 16].astype(np.float64) * 0.01  # us
+    ok = rt[:, 0] > 0
+    rt = rt[ok]
+    t0 = rt[:, 0].min()
+    rt = rt - t0
+    start, end = rt[:, 0], rt[:, 10]
+    nb = int(np.ceil(end.max())) + 1
+    def occ(a, b):
+        h = np.zeros(nb)
+        for x, y in zip(rt[:, a], rt[:, b]):
+            i0, i1 = int(x), int(y)
+            for i in range(i0, min(i1, nb - 1) + 1):
+                h[i] += max(0.0, min(y, i + 1) - max(x, i))  # wave-us inside bin i
+        return h
+    return {"span_us": float(end.max()), "start_us": np.percentile(start, [50, 95, 100]).tolist(),
+            "end_us": np.percentile(end, [5, 50, 95, 100]).tolist(),
+            "dur_us": np.percentile(end - start, [50, 95, 100]).tolist(),
+            "load": occ(0, 1), "physics": occ(2, 5), "outputs": occ(6, 10)}
+
+
+def summarise_timeline(tl):
+    import numpy as np
+    nb = max(len(t["load"]) for t in tl)
+    pad = lambda v: np.pad(v, (0, nb - len(v)))  # noqa: E731
+    return {"span_us_mean": float(np.mean([t["span_us"] for t in tl])),
+            "wave_start_us_p50_p95_max": np.mean([t["start_us"] for t in tl], axis=0).round(2).tolist(),
+            "wave_end_us_p5_p50_p95_max": np.mean([t["end_us"] for t in tl], axis=0).round(2).tolist(),
+            "wave_duration_us_p50_p95_max": np.mean([t["dur_us"] for t in tl], axis=0).round(2).tolist(),
+            "waves_in_phase_per_us_bin": {k: np.mean([pad(t[k]) for t in tl], axis=0).round(0).tolist()
+                                          for k in ("load", "physics", "outputs")}}
 
 
 def build(extra=()):
@@ -50,12 +87,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=0, help="untimed steps first (1000: steady state)")
     ap.add_argument("--out", default="")
     ap.add_argument("--lane-group", type=int, default=None, help="SoccerBatch.set_lane_group(G) (ms_set_lane_group)")
+    ap.add_argument("--lib", default=STAMP_LIB, help="a -DMS_STAMPS library (default: the product stamps build)")
     a, extra = ap.parse_known_args()
     sys.path.insert(0, PKG)
     if a.build:
         build(extra)
         return
-    os.environ["MARL_SOCCER_LIB"] = STAMP_LIB
+    os.environ["MARL_SOCCER_LIB"] = a.lib
     import numpy as np
     import torch
     from marlsoccer import SoccerBatch, _native
@@ -78,6 +116,7 @@ def main():
     seg = {k: [] for k in ORDER[1:]}
     seg_slow = {k: [] for k in ORDER[1:]}
     spans, totals, slow_tot, maxnc, worst, accs = [], [], [], [], [], []
+    tl = []  # per sampled launch: the real-time timeline (every XCD's waves on one clock)
     for t in range(a.warmup):
         acts.uniform_(-1.0, 1.0, generator=g)
         env.step(acts)
@@ -99,6 +138,8 @@ def main():
             for i in range(1, len(ORDER)):  # carry forward stamps of untaken branches
                 k, prev = ORDER[i], ORDER[i - 1]
                 st[:, k] = np.where(st[:, k] == 0, st[:, prev], st[:, k])
+                st[:, RT + k] = np.where(st[:, RT + k] == 0, st[:, RT + prev], st[:, RT + k])
+            tl.append(timeline(st))
             tot = st[:, 10] - st[:, 0]
             slow = tot >= np.quantile(tot, 0.95)
             totals.append(tot.mean())
@@ -117,7 +158,8 @@ def main():
     res = {"envs": a.envs, "steps": a.steps, "warmup": a.warmup, "samples": len(totals),
            "launch": f"lane groups, {env.lane_group} lanes per env" if env.lane_group > 0 else "one wave per 64-env block",
            "wave_cycles_mean": float(np.mean(totals)), "wave_cycles_slowest5pct": float(np.mean(slow_tot)),
-           "launch_span_cycles": float(np.mean(spans)),
+           "launch_span_cycles_note": "s_memtime counters differ between XCDs: see timeline (real time)",
+           "timeline": summarise_timeline(tl),
            "worst_wave_cycles_mean": float(np.mean([w["cycles"] for w in worst])),
            "worst_wave_max_contacts": {str(v): sum(1 for w in worst if w["max_contacts"] == v) for v in sorted({w["max_contacts"] for w in worst})},
            "narrowphase_acc_mean": {ACC[16 + j]: round(float(np.mean(np.concatenate(accs)[:, j])), 1) for j in range(6)},

@@ -15,7 +15,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "marl-soccer_amd")
-VDIR = os.path.join(PKG, "lib", "variants")
+# this round's experiment libraries (lib/variants holds older ones and is not shipped: .gpurunignore)
+VDIR = os.environ.get("MS_VARIANTS_DIR", os.path.join(PKG, "lib", "exp"))
 sys.path.insert(0, PKG)
 
 
@@ -24,6 +25,8 @@ def build(name, defs, src=None):
     os.makedirs(VDIR, exist_ok=True)
     out = os.path.join(VDIR, f"lib_{name}.so")
     srcs = [src] + build_native.SOURCES[1:] if src else build_native.SOURCES
+    if "-DMS_PAIR_ONLY" in defs.split():  # lane-pair kernels only, no policy kernels: a 20-s build
+        srcs = srcs[:1]
     cmd = [build_native.hipcc(), *build_native.FLAGS, *defs.split(), "-o", out, *srcs]
     subprocess.run(cmd, check=True)
     print("built", out)
