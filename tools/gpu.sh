@@ -167,6 +167,20 @@ vstamps() {  # tag lib-name envs: per-phase stamps of a -DMS_STAMPS lib/exp vari
   python -c "import json; d=json.load(open('$O/stamps_$2_$3.json')); print('$2', $3, 'mean', round(d['wave_cycles_mean']), 'slow5', round(d['wave_cycles_slowest5pct']), 'worst', round(d.get('worst_wave_cycles_mean', 0)), {k: round(v['mean']) for k, v in d['phases'].items()}); t=d['timeline']; print({k: v for k, v in t.items() if k != 'waves_in_phase_per_us_bin'})"
 }
 
+tcc() {  # tag lib-name: HBM request-size split of the lane-pair step kernel (tools/tcc_split.py), steady window
+  local T=$1 V=$2 i=0 P
+  local O=gpurun_out/$T/tcc_$V; mkdir -p $O
+  local LIB=marl-soccer_amd/lib/exp/lib_$V.so
+  [ "$V" = product ] && LIB=marl-soccer_amd/lib/libmarlsoccer.so
+  for P in "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_EA0_WRREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_sum TCC_BUBBLE_sum"; do
+    i=$((i+1))
+    MARL_SOCCER_LIB=$LIB timeout -s KILL 200 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- python bench.py --envs 65536 --warmup 1000 --steps 200 --no-cpu-baseline --no-ring-leg --fused 0 > $O/p$i.log 2>&1 \
+      || { echo "tcc pass $i failed"; tail -5 $O/p$i.log; return 1; }
+  done
+  python tools/tcc_split.py $O ms_step_pair_kernel 65536 200 | tee $O/summary.json
+  rm -rf $O/p1/*/*.csv.tmp 2>/dev/null; true
+}
+
 driver() {  # the driver's own bench command, N = 1 (BENCH_rNN.json)
   local O=gpurun_out/$1; mkdir -p $O
   timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err \
