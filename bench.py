@@ -70,6 +70,9 @@ def parse():
                     help="ms_step kernel (SoccerBatch.set_lane_group): G = 2, 8 or 16 lanes per env, 0 one lane "
                          "per env, -1 automatic; default: the library's (8 lanes while envs x 8 fit the SIMDs, "
                          "else 2)")
+    ap.add_argument("--generic", action="store_true",
+                    help="a non-default reward config (ball_proximity_multiplier 0.003, same physics): times the generic "
+                         "<false> kernels, whose multipliers come from the kernel arguments")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ring-leg", action="store_true", help="skip the frame-ring leg timed beside the headline")
     ap.add_argument("--fused", type=int, default=50, metavar="K",
@@ -244,10 +247,12 @@ def main():
 
     E = args.envs
     cfg = None
-    if args.max_steps != 1000:
+    if args.max_steps != 1000 or args.generic:
         from marlsoccer.config import load_config
         cfg = load_config()
         cfg["simulation"]["max_steps"] = args.max_steps
+        if args.generic:
+            cfg["rewards"]["ball_proximity_multiplier"] = 0.003
     ring = args.frame_ring
     if ring and args.allgather:
         raise SystemExit("--frame-ring and --allgather are exclusive")
@@ -506,7 +511,8 @@ def main():
             "dtype": "f32",
             "data": f"synthetic: uniform(-1,1) fp32 actions (device Philox, {nsets} distinct (E,4,3) buffers "
                     f"for {args.warmup + args.steps} steps, read from HBM each step); env i seeded 19+i; "
-                    "default config.json physics/rewards" + (f", max_steps={args.max_steps}" if args.max_steps != 1000 else ""),
+                    ("config.json physics, rewards with ball_proximity_multiplier 0.003 (generic kernel)" if args.generic
+                     else "default config.json physics/rewards") + (f", max_steps={args.max_steps}" if args.max_steps != 1000 else ""),
             "config": {"workload": f"{E} parallel envs per MI355X" +
                                    (" (BASELINE.json configs[2])" if E == 65536 and args.max_steps == 1000 else
                                     " (BASELINE.json configs[1])" if E == 4096 and args.max_steps == 1000 else

@@ -1633,6 +1633,7 @@ __global__ __launch_bounds__(MS_BLOCK) void ms_step_ring_kernel(DevState S, Para
   }
 }
 
+#ifndef MS_KSTEP_TU  // (ms_kstep.hip includes this file for the device code of the K-step kernels only)
 __global__ __launch_bounds__(MS_BLOCK) void ms_reset_kernel(DevState S, Params P, const uint64_t* __restrict__ pcg,
                                                             const uint8_t* __restrict__ mask, int mode, int set_hist_empty,
                                                             float* __restrict__ obs, const Ring rg) {
@@ -1779,11 +1780,19 @@ __global__ void ms_debug_rewards_kernel(Params P, int64_t n, const float* __rest
   rew[2 * e + 1] = r;
 }
 
+#endif  // MS_KSTEP_TU
+
 // small batches: one env per lane group (ms_step when envs x 8 <= the device's lanes)
 #include "ms_group.inc"
 // two lanes per env, two waves per SIMD
 #include "ms_pair.inc"
 
+// ms_kstep.hip: launch the K-step kernel of lane group G (2: lane pairs; 8, 16: lane groups) on stream st
+hipError_t ms_kstep_launch(int G, bool default_params, dim3 grid, hipStream_t st, const DevState& S, const Params& P, int K,
+                           const float* actions, float* obs, float* rew, uint8_t* term, uint8_t* trunc, int8_t* goal,
+                           int32_t* score, Counters* ctr, int group_solve);
+
+#ifndef MS_KSTEP_TU
 // =============================================================================================
 // Host side: the C-ABI
 // =============================================================================================
@@ -2144,40 +2153,18 @@ int ms_step_n(ms_env* h, int K, const float* actions, float* obs, float* rew, ui
   if (((uintptr_t)actions & 15u) || ((uintptr_t)obs & 7u) || ((uintptr_t)rew & 15u) || ((uintptr_t)term & 3u) ||
       ((uintptr_t)trunc & 3u) || ((uintptr_t)score & 7u))
     return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_n: misaligned buffer (actions/rew 16 B, obs/score 8 B, flags 4 B)");
-  if (h->group == 2) {
-    const dim3 grid(grid_for(h->n, pr::EPW));
-    if (h->default_params)
-      hipLaunchKernelGGL(ms_step_pair_n_kernel<true>, grid, dim3(64), 0, h->stream, h->S, h->P, K, actions, obs, rew,
-                         term, trunc, goal, score, h->ctr);
-    else
-      hipLaunchKernelGGL(ms_step_pair_n_kernel<false>, grid, dim3(64), 0, h->stream, h->S, h->P, K, actions, obs, rew,
-                         term, trunc, goal, score, h->ctr);
-    HIPCHK(hipGetLastError());
-    return MS_OK;
-  }
-#ifndef MS_PAIR_ONLY
-  if (h->group > 0) {
-    const int G = h->group;
-    const dim3 grid(grid_for(h->n, 64 / G));
-    if (G == 8) {
-      if (h->default_params)
-        hipLaunchKernelGGL((ms_step_group_n_kernel<true, 8>), grid, dim3(64), 0, h->stream, h->S, h->P, K, actions, obs,
-                           rew, term, trunc, goal, score, h->ctr, h->group_solve);
-      else
-        hipLaunchKernelGGL((ms_step_group_n_kernel<false, 8>), grid, dim3(64), 0, h->stream, h->S, h->P, K, actions,
-                           obs, rew, term, trunc, goal, score, h->ctr, h->group_solve);
-    } else {
-      if (h->default_params)
-        hipLaunchKernelGGL((ms_step_group_n_kernel<true, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, K, actions,
-                           obs, rew, term, trunc, goal, score, h->ctr, h->group_solve);
-      else
-        hipLaunchKernelGGL((ms_step_group_n_kernel<false, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, K, actions,
-                           obs, rew, term, trunc, goal, score, h->ctr, h->group_solve);
-    }
-    HIPCHK(hipGetLastError());
-    return MS_OK;
-  }
+  // the K-step kernels live in their own translation unit (ms_kstep.hip, built without machine LICM)
+  const int G = h->group;
+#ifdef MS_PAIR_ONLY
+  if (G == 2) {
+#else
+  if (G == 2 || G == 8 || G == 16) {
 #endif
+    const dim3 grid(grid_for(h->n, G == 2 ? pr::EPW : 64 / G));
+    HIPCHK(ms_kstep_launch(G, h->default_params, grid, h->stream, h->S, h->P, K, actions, obs, rew, term, trunc, goal,
+                           score, h->ctr, h->group_solve));
+    return MS_OK;
+  }
   const int64_t n = h->n;
   for (int k = 0; k < K; ++k) {
     const int64_t o = (int64_t)k * n;
@@ -2337,3 +2324,4 @@ int ms_reset_stats(ms_env* h) {
 }
 
 }  // extern "C"
+#endif  // MS_KSTEP_TU

@@ -22,7 +22,7 @@ def main(tag, extra=()):
     flags = [f for f in build_native.FLAGS if f not in ("-shared",)]
     out = ""
     for src in build_native.SOURCES:
-        cmd = [build_native.hipcc(), *flags, *extra, "-Rpass-analysis=kernel-resource-usage", "--cuda-device-only",
+        cmd = [build_native.hipcc(), *flags, *extra, *build_native.unit_flags(src), "-Rpass-analysis=kernel-resource-usage", "--cuda-device-only",
                "-c", "-o", os.devnull, src]
         out += subprocess.run(cmd, capture_output=True, text=True, check=True).stderr
     lines = []

@@ -73,9 +73,7 @@ def summarise_timeline(tl):
 def build(extra=()):
     import build_native
     os.makedirs(os.path.dirname(STAMP_LIB), exist_ok=True)
-    cmd = [build_native.hipcc(), *build_native.FLAGS, "-DMS_STAMPS", *extra, "-o", STAMP_LIB, *build_native.SOURCES]
-    print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    build_native.compile_and_link(STAMP_LIB, build_native.SOURCES, extra=["-DMS_STAMPS", *extra], verbose=True)
 
 
 def main():

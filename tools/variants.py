@@ -20,15 +20,16 @@ VDIR = os.environ.get("MS_VARIANTS_DIR", os.path.join(PKG, "lib", "exp"))
 sys.path.insert(0, PKG)
 
 
-def build(name, defs, src=None):
+def build(name, defs, csrc=None):
+    """lib_NAME.so from the csrc directory (default: the working tree's) with -D flags `defs`;
+    -DMS_PAIR_ONLY: the lane-pair kernels only (no policy kernels), a short build."""
     import build_native
     os.makedirs(VDIR, exist_ok=True)
     out = os.path.join(VDIR, f"lib_{name}.so")
-    srcs = [src] + build_native.SOURCES[1:] if src else build_native.SOURCES
-    if "-DMS_PAIR_ONLY" in defs.split():  # lane-pair kernels only, no policy kernels: a 20-s build
-        srcs = srcs[:1]
-    cmd = [build_native.hipcc(), *build_native.FLAGS, *defs.split(), "-o", out, *srcs]
-    subprocess.run(cmd, check=True)
+    d = csrc or build_native.CSRC
+    names = ["ms_env.hip", "ms_kstep.hip"] if "-DMS_PAIR_ONLY" in defs.split() else ["ms_env.hip", "ms_policy.hip", "ms_kstep.hip"]
+    srcs = [os.path.join(d, n) for n in names if os.path.exists(os.path.join(d, n))]  # older revisions: no ms_kstep.hip
+    build_native.compile_and_link(out, srcs, extra=defs.split())
     print("built", out)
 
 
@@ -49,7 +50,7 @@ def main():
             arc = subprocess.run(["git", "-C", ROOT, "archive", rev, "marl-soccer_amd/csrc", "include"],
                                  check=True, capture_output=True).stdout
             subprocess.run(["tar", "-x", "-C", tmp], input=arc, check=True)
-            build(name, defs, os.path.join(tmp, "marl-soccer_amd", "csrc", "ms_env.hip"))
+            build(name, defs, os.path.join(tmp, "marl-soccer_amd", "csrc"))
         finally:
             shutil.rmtree(tmp)
     elif a[0] == "run":
