@@ -510,7 +510,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic: uniform(-1,1) fp32 actions (device Philox, {nsets} distinct (E,4,3) buffers "
-                    f"for {args.warmup + args.steps} steps, read from HBM each step); env i seeded 19+i; "
+                    f"for {args.warmup + args.steps} steps, read from HBM each step); env i seeded 19+i; " +
                     ("config.json physics, rewards with ball_proximity_multiplier 0.003 (generic kernel)" if args.generic
                      else "default config.json physics/rewards") + (f", max_steps={args.max_steps}" if args.max_steps != 1000 else ""),
             "config": {"workload": f"{E} parallel envs per MI355X" +

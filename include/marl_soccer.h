@@ -187,10 +187,12 @@ typedef struct ms_env ms_env;
 /* Fill `cfg` with the reference defaults (config.json + code defaults). */
 void ms_config_default(ms_config *cfg);
 
-/* 1 when `cfg` selects the step kernel specialised for the reference's default physics and
- * rewards (config.json, compile-time constants; only max_steps and autoreset may differ),
- * 0 when the generic kernel (parameters from kernel arguments) runs; negative on error.
- * Both kernels compute the same results. Host-only, no device needed. */
+/* Which step-kernel specialisation `cfg` selects: 1 = the reference's default physics and
+ * rewards as compile-time constants (config.json; only max_steps and autoreset may differ),
+ * 2 = the default physics as constants with the reward multipliers from the kernel arguments
+ * (lane-pair and lane-group kernels; the one-lane and frame-ring kernels run generic for it),
+ * 0 = the generic kernel (every parameter from the kernel arguments); negative on error.
+ * Every kernel computes the same results. Host-only, no device needed. */
 int ms_config_specialised(const ms_config *cfg);
 
 /* Allocate device state for `n_envs` environments on HIP device `device`; launches

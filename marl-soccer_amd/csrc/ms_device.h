@@ -56,9 +56,11 @@ __device__ __forceinline__ float vdot(V2 a, V2 b) { const V2 p = a * b; return p
 __device__ __forceinline__ float vcross(V2 a, V2 b) { const V2 p = a * b.yx; return p.x - p.y; }
 __device__ __forceinline__ V2 vperp(V2 a) { return v2(-a.y, a.x); }
 // (a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x) with the outer add fused (solver impulses only;
-// the fp32 oracle's vrotate is the same SMADD form); x * -1 is an exact sign flip
+// the fp32 oracle's vrotate is the same SMADD form). The low product's sign comes from its
+// multiplicand, (-a.y) * b.y = -(a.y * b.y) exactly, which is off the solver's dependency chain (a
+// is the contact normal), instead of a multiply of the product by (-1, 1) on it
 __device__ __forceinline__ V2 vrotate(V2 a, V2 b) {
-  return __builtin_elementwise_fma(V2{a.x, a.x}, b, (a.y * b.yx) * V2{-1.0f, 1.0f});
+  return __builtin_elementwise_fma(V2{a.x, a.x}, b, V2{-a.y, a.y} * b.yx);
 }
 __device__ __forceinline__ float vlengthsq(V2 a) { return vdot(a, a); }
 __device__ __forceinline__ float fmaxr(float a, float b) { return (a > b) ? a : b; }  // cpfmax

@@ -1346,6 +1346,31 @@ __host__ __device__ constexpr Params default_params() {
      {10.0f, 225.0f, 10.0f, 375.0f, -1.0f, 0.0f, 1.0f, {9.0f, 224.0f, 11.0f, 376.0f}},
      {790.0f, 225.0f, 790.0f, 375.0f, -1.0f, 0.0f, 1.0f, {789.0f, 224.0f, 791.0f, 376.0f}}}};
 }
+
+// The parameters a step kernel computes with, by its specialisation mode PM (ms_config_specialised):
+// 1 = the reference's defaults as compile-time constants, 2 = the default physics as constants with
+// the reward multipliers from the kernel arguments (a reward-shaping config keeps the physics folded
+// into the instructions), 0 = everything from the kernel arguments. max_steps and autoreset are
+// always runtime values.
+template <int PM>
+__device__ __forceinline__ Params kernel_params(const Params& Pin) {
+  if constexpr (PM == 0) {
+    return Pin;
+  } else {
+    Params P = default_params();
+    P.max_steps = Pin.max_steps;
+    P.autoreset = Pin.autoreset;
+    if constexpr (PM == 2) {
+      P.prox_mult = Pin.prox_mult;
+      P.goal_mult = Pin.goal_mult;
+      P.alive = Pin.alive;
+      P.goal_reward = Pin.goal_reward;
+      P.concede_penalty = Pin.concede_penalty;
+      P.score_diff_mult = Pin.score_diff_mult;
+    }
+    return P;
+  }
+}
 // The first HBM batch of one state block (one wave's 64 envs): scalars, bodies, actions, the
 // previous step's arbiter-cache entries 0..KC-1 and PCG64. The scalars come first and alone
 // (fetch_scalars): the cache entries' addresses depend on them (parity bit, entry count).
@@ -1788,7 +1813,7 @@ __global__ void ms_debug_rewards_kernel(Params P, int64_t n, const float* __rest
 #include "ms_pair.inc"
 
 // ms_kstep.hip: launch the K-step kernel of lane group G (2: lane pairs; 8, 16: lane groups) on stream st
-hipError_t ms_kstep_launch(int G, bool default_params, dim3 grid, hipStream_t st, const DevState& S, const Params& P, int K,
+hipError_t ms_kstep_launch(int G, int param_mode, dim3 grid, hipStream_t st, const DevState& S, const Params& P, int K,
                            const float* actions, float* obs, float* rew, uint8_t* term, uint8_t* trunc, int8_t* goal,
                            int32_t* score, Counters* ctr, int group_solve);
 
@@ -1805,6 +1830,7 @@ struct ms_env {
   int64_t lanes;   // the device's wave slots at one wave per SIMD x 64 (4 x CUs x 64)
   Params P;
   bool default_params;  // P == default_params() up to max_steps/autoreset: specialised kernel
+  int param_mode;       // kernel_params' mode of the lane-pair and lane-group kernels (2: default physics)
   DevState S;
   void* mem;
   Counters* ctr;
@@ -1968,12 +1994,26 @@ static bool params_are_default(const Params& P) {
   d.autoreset = P.autoreset;
   return memcmp(&d, &P, sizeof(Params)) == 0;
 }
+// kernel_params' mode for P: 1 all default, 2 default physics (any reward multipliers), 0 otherwise
+static int param_mode(const Params& P) {
+  if (params_are_default(P)) return 1;
+  Params d = default_params();
+  d.max_steps = P.max_steps;
+  d.autoreset = P.autoreset;
+  d.prox_mult = P.prox_mult;
+  d.goal_mult = P.goal_mult;
+  d.alive = P.alive;
+  d.goal_reward = P.goal_reward;
+  d.concede_penalty = P.concede_penalty;
+  d.score_diff_mult = P.score_diff_mult;
+  return memcmp(&d, &P, sizeof(Params)) == 0 ? 2 : 0;
+}
 
 int ms_config_specialised(const ms_config* cfg) {
   if (!cfg) return fail(MS_ERR_INVALID_ARGUMENT, "ms_config_specialised: null config") * -1;
   Params P;
   make_params(cfg, &P);
-  return params_are_default(P) ? 1 : 0;
+  return param_mode(P);
 }
 
 static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
@@ -1998,6 +2038,7 @@ int ms_create(const ms_config* cfg, int64_t n_envs, int device, void* stream, ms
   if (cfg) h->cfg = *cfg; else ms_config_default(&h->cfg);
   make_params(&h->cfg, &h->P);
   h->default_params = params_are_default(h->P);
+  h->param_mode = param_mode(h->P);
   {  // ms_step's default kernel by batch size (auto_group)
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
@@ -2104,11 +2145,14 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
   [[maybe_unused]] const unsigned nblk = grid_for(h->n, MS_BLOCK);
   if (h->group == 2) {
     const dim3 grid(grid_for(h->n, pr::EPW));
-    if (h->default_params)
-      hipLaunchKernelGGL(ms_step_pair_kernel<true>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew, term,
+    if (h->param_mode == 1)
+      hipLaunchKernelGGL(ms_step_pair_kernel<1>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew, term,
+                         trunc, goal, score, h->ctr);
+    else if (h->param_mode == 2)
+      hipLaunchKernelGGL(ms_step_pair_kernel<2>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew, term,
                          trunc, goal, score, h->ctr);
     else
-      hipLaunchKernelGGL(ms_step_pair_kernel<false>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew,
+      hipLaunchKernelGGL(ms_step_pair_kernel<0>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew,
                          term, trunc, goal, score, h->ctr);
   } else {
 #ifdef MS_PAIR_ONLY  // experiment builds (tools/variants.py): the lane-pair kernels only
@@ -2117,21 +2161,19 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
   if (h->group > 0) {
     const int G = h->group;
     const dim3 grid(grid_for(h->n, 64 / G));
+#define MS_GROUP_LAUNCH(PM, GG)                                                                                  \
+  hipLaunchKernelGGL((ms_step_group_kernel<PM, GG>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew, term, \
+                     trunc, goal, score, h->ctr, h->group_solve)
     if (G == 8) {
-      if (h->default_params)
-        hipLaunchKernelGGL((ms_step_group_kernel<true, 8>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew,
-                           term, trunc, goal, score, h->ctr, h->group_solve);
-      else
-        hipLaunchKernelGGL((ms_step_group_kernel<false, 8>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs,
-                           rew, term, trunc, goal, score, h->ctr, h->group_solve);
+      if (h->param_mode == 1) MS_GROUP_LAUNCH(1, 8);
+      else if (h->param_mode == 2) MS_GROUP_LAUNCH(2, 8);
+      else MS_GROUP_LAUNCH(0, 8);
     } else {
-      if (h->default_params)
-        hipLaunchKernelGGL((ms_step_group_kernel<true, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs,
-                           rew, term, trunc, goal, score, h->ctr, h->group_solve);
-      else
-        hipLaunchKernelGGL((ms_step_group_kernel<false, 16>), grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs,
-                           rew, term, trunc, goal, score, h->ctr, h->group_solve);
+      if (h->param_mode == 1) MS_GROUP_LAUNCH(1, 16);
+      else if (h->param_mode == 2) MS_GROUP_LAUNCH(2, 16);
+      else MS_GROUP_LAUNCH(0, 16);
     }
+#undef MS_GROUP_LAUNCH
   } else if (h->default_params) {
     hipLaunchKernelGGL(ms_step_kernel<true>, dim3(nblk), dim3(MS_BLOCK), 0, h->stream, h->S, h->P, actions, obs, rew,
                        term, trunc, goal, score, h->ctr);
@@ -2161,7 +2203,7 @@ int ms_step_n(ms_env* h, int K, const float* actions, float* obs, float* rew, ui
   if (G == 2 || G == 8 || G == 16) {
 #endif
     const dim3 grid(grid_for(h->n, G == 2 ? pr::EPW : 64 / G));
-    HIPCHK(ms_kstep_launch(G, h->default_params, grid, h->stream, h->S, h->P, K, actions, obs, rew, term, trunc, goal,
+    HIPCHK(ms_kstep_launch(G, h->param_mode, grid, h->stream, h->S, h->P, K, actions, obs, rew, term, trunc, goal,
                            score, h->ctr, h->group_solve));
     return MS_OK;
   }

@@ -8,34 +8,33 @@
 #define MS_KSTEP_TU 1
 #include "ms_env.hip"
 
-hipError_t ms_kstep_launch(int G, bool default_params, dim3 grid, hipStream_t st, const DevState& S, const Params& P, int K,
+hipError_t ms_kstep_launch(int G, int param_mode, dim3 grid, hipStream_t st, const DevState& S, const Params& P, int K,
                            const float* actions, float* obs, float* rew, uint8_t* term, uint8_t* trunc, int8_t* goal,
                            int32_t* score, Counters* ctr, int group_solve) {
+#define MS_PAIR_N(PM)                                                                                              \
+  hipLaunchKernelGGL(ms_step_pair_n_kernel<PM>, grid, dim3(64), 0, st, S, P, K, actions, obs, rew, term, trunc, goal, \
+                     score, ctr)
+#define MS_GROUP_N(PM, GG)                                                                                           \
+  hipLaunchKernelGGL((ms_step_group_n_kernel<PM, GG>), grid, dim3(64), 0, st, S, P, K, actions, obs, rew, term, trunc, \
+                     goal, score, ctr, group_solve)
   if (G == 2) {
-    if (default_params)
-      hipLaunchKernelGGL(ms_step_pair_n_kernel<true>, grid, dim3(64), 0, st, S, P, K, actions, obs, rew, term, trunc, goal,
-                         score, ctr);
-    else
-      hipLaunchKernelGGL(ms_step_pair_n_kernel<false>, grid, dim3(64), 0, st, S, P, K, actions, obs, rew, term, trunc,
-                         goal, score, ctr);
+    if (param_mode == 1) MS_PAIR_N(1);
+    else if (param_mode == 2) MS_PAIR_N(2);
+    else MS_PAIR_N(0);
 #ifndef MS_PAIR_ONLY
   } else if (G == 8) {
-    if (default_params)
-      hipLaunchKernelGGL((ms_step_group_n_kernel<true, 8>), grid, dim3(64), 0, st, S, P, K, actions, obs, rew, term, trunc,
-                         goal, score, ctr, group_solve);
-    else
-      hipLaunchKernelGGL((ms_step_group_n_kernel<false, 8>), grid, dim3(64), 0, st, S, P, K, actions, obs, rew, term,
-                         trunc, goal, score, ctr, group_solve);
+    if (param_mode == 1) MS_GROUP_N(1, 8);
+    else if (param_mode == 2) MS_GROUP_N(2, 8);
+    else MS_GROUP_N(0, 8);
   } else if (G == 16) {
-    if (default_params)
-      hipLaunchKernelGGL((ms_step_group_n_kernel<true, 16>), grid, dim3(64), 0, st, S, P, K, actions, obs, rew, term,
-                         trunc, goal, score, ctr, group_solve);
-    else
-      hipLaunchKernelGGL((ms_step_group_n_kernel<false, 16>), grid, dim3(64), 0, st, S, P, K, actions, obs, rew, term,
-                         trunc, goal, score, ctr, group_solve);
+    if (param_mode == 1) MS_GROUP_N(1, 16);
+    else if (param_mode == 2) MS_GROUP_N(2, 16);
+    else MS_GROUP_N(0, 16);
 #endif
   } else {
     return hipErrorInvalidValue;
   }
+#undef MS_PAIR_N
+#undef MS_GROUP_N
   return hipGetLastError();
 }

@@ -174,13 +174,15 @@ def default_config() -> MsConfig:
     return cfg
 
 
-def config_specialised(cfg: MsConfig) -> bool:
-    """True when `cfg` runs the step kernel specialised for the reference's default physics
-    and rewards (compile-time constants); False: the generic kernel. Same results either way."""
+def config_specialised(cfg: MsConfig) -> int:
+    """The step-kernel specialisation `cfg` selects (ms_config_specialised): 1 = the reference's
+    default physics and rewards as compile-time constants, 2 = the default physics with runtime
+    reward multipliers (lane-pair and lane-group kernels), 0 = the generic kernel. Same results
+    in every case."""
     rc = lib().ms_config_specialised(C.byref(cfg))
     if rc < 0:
         check(-rc, "ms_config_specialised")
-    return rc == 1
+    return int(rc)
 
 
 def _seed_words(seed: int) -> np.ndarray:

@@ -313,9 +313,9 @@ class SoccerBatch:
         return out
 
     @property
-    def specialised(self) -> bool:
-        """True when ms_step runs the kernel compiled for the reference's default physics and
-        rewards (ms_config_specialised)."""
+    def specialised(self) -> int:
+        """The step kernel's specialisation (ms_config_specialised): 1 = compiled for the reference's
+        default physics and rewards, 2 = default physics with runtime reward multipliers, 0 = generic."""
         return N.config_specialised(self._cfg)
 
     def export_state_raw(self) -> torch.Tensor:

@@ -62,3 +62,14 @@ def test_launch_label_names_the_lane_pair_kernel(bench):
     assert bench.launch_label(2).startswith("lane pairs, 2 lanes per env (32 envs per wave")
     assert bench.launch_label(8) == "lane groups, 8 lanes per env (8 envs per wave)"
     assert bench.launch_label(0).startswith("one lane per env")
+
+
+def test_bench_source_compiles_without_warnings():
+    """bench.py's JSON-line strings are built by implicit concatenation; a missing '+' before a
+    parenthesised part turns it into a call that only fails on the GPU box (SyntaxWarning here)."""
+    import warnings
+    with open(os.path.join(ROOT, "bench.py")) as f:
+        src = f.read()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        compile(src, "bench.py", "exec")

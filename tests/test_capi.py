@@ -43,9 +43,9 @@ def test_abi_version_and_config_defaults():
 
 
 def test_default_config_selects_specialised_step_kernel():
-    """ms_create launches the constant-folded step kernel only for parameters equal, bit for
-    bit, to the reference's defaults (max_steps/autoreset excepted); anything else runs the
-    generic kernel."""
+    """ms_create launches the constant-folded step kernel for parameters equal, bit for bit, to the
+    reference's defaults (max_steps/autoreset excepted), the default-physics kernel for configs
+    that change reward multipliers only, and the generic kernel for anything else."""
     from marlsoccer import _native as N
     from marlsoccer.config import load_config, to_ms_config
     assert N.config_specialised(N.default_config())
@@ -54,11 +54,16 @@ def test_default_config_selects_specialised_step_kernel():
     assert N.config_specialised(to_ms_config(cfg, False))
     cfg["simulation"]["max_steps"] = 70
     assert N.config_specialised(to_ms_config(cfg, True))
-    for sect, key, val in (("rewards", "score_difference_multiplier", 5.0), ("rewards", "goal_conceded_penalty", 1.0),
-                           ("physics", "ball_mass", 2.0), ("physics", "max_velocity", 150.0)):
+    assert N.config_specialised(N.default_config()) == 1
+    # reward multipliers only: the default physics stays compile-time (mode 2); any physics value: generic
+    for sect, key, val, mode in (("rewards", "score_difference_multiplier", 5.0, 2),
+                                 ("rewards", "goal_conceded_penalty", 1.0, 2),
+                                 ("rewards", "ball_proximity_multiplier", 0.003, 2),
+                                 ("physics", "ball_mass", 2.0, 0), ("physics", "max_velocity", 150.0, 0),
+                                 ("physics", "action_torque_max", 800.0, 0)):
         c = load_config()
         c[sect][key] = val
-        assert not N.config_specialised(to_ms_config(c, True)), key
+        assert N.config_specialised(to_ms_config(c, True)) == mode, key
 
 
 @pytest.mark.parametrize("seed", [0, 1, 19, 123456, 2 ** 32 - 1, 2 ** 32, 2 ** 40 + 7, 2 ** 64 - 1, 2 ** 70 + 3])

@@ -161,6 +161,15 @@ vrun() {  # tag name...: time lib/exp variants (tools/variants.py run), steady w
   cat $O/variants.txt $O/variants_driver.txt
 }
 
+vrunn() {  # tag envs name...: vrun at another batch size (steady window, twice)
+  local O=gpurun_out/$1 N=$2; shift 2; mkdir -p $O
+  local r
+  for r in 1 2; do
+    timeout -k 10 600 python tools/variants.py run --envs $N "$@" >> $O/variants_$N.txt 2>&1 || { tail -20 $O/variants_$N.txt; return 1; }
+  done
+  cat $O/variants_$N.txt
+}
+
 vstamps() {  # tag lib-name envs: per-phase stamps of a -DMS_STAMPS lib/exp variant
   local O=gpurun_out/$1; mkdir -p $O
   timeout -k 10 240 python tools/stamps.py --lib marl-soccer_amd/lib/exp/lib_$2.so --envs $3 --steps 300 --warmup 1000 --every 10 --out $O/stamps_$2_$3.json > $O/stamps_$2_$3.log 2>&1 || { tail $O/stamps_$2_$3.log; return 1; }
@@ -178,7 +187,7 @@ tcc() {  # tag lib-name: HBM request-size split of the lane-pair step kernel (to
       || { echo "tcc pass $i failed"; tail -5 $O/p$i.log; return 1; }
   done
   python tools/tcc_split.py $O ms_step_pair_kernel 65536 200 | tee $O/summary.json
-  rm -rf $O/p1/*/*.csv.tmp 2>/dev/null; true
+  rm -rf $O/p1 $O/p2  # the raw per-dispatch CSVs exceed gpurun's 64-MiB copy-back
 }
 
 driver() {  # the driver's own bench command, N = 1 (BENCH_rNN.json)
