@@ -172,13 +172,13 @@ vrunn() {  # tag envs name...: vrun at another batch size (steady window, twice)
 
 vstamps() {  # tag lib-name envs: per-phase stamps of a -DMS_STAMPS lib/exp variant
   local O=gpurun_out/$1; mkdir -p $O
-  timeout -k 10 240 python tools/stamps.py --lib marl-soccer_amd/lib/exp/lib_$2.so --envs $3 --steps 300 --warmup 1000 --every 10 --out $O/stamps_$2_$3.json > $O/stamps_$2_$3.log 2>&1 || { tail $O/stamps_$2_$3.log; return 1; }
+  timeout -k 10 240 python tools/stamps.py --fine --lib marl-soccer_amd/lib/exp/lib_$2.so --envs $3 --steps 300 --warmup 1000 --every 10 --out $O/stamps_$2_$3.json > $O/stamps_$2_$3.log 2>&1 || { tail $O/stamps_$2_$3.log; return 1; }
   python -c "import json; d=json.load(open('$O/stamps_$2_$3.json')); print('$2', $3, 'mean', round(d['wave_cycles_mean']), 'slow5', round(d['wave_cycles_slowest5pct']), 'worst', round(d.get('worst_wave_cycles_mean', 0)), {k: round(v['mean']) for k, v in d['phases'].items()}); t=d['timeline']; print({k: v for k, v in t.items() if k != 'waves_in_phase_per_us_bin'})"
 }
 
 vstampsd() {  # tag lib-name envs: the same over the driver's window (warm-up 5, 20 steps, every launch)
   local O=gpurun_out/$1; mkdir -p $O
-  timeout -k 10 240 python tools/stamps.py --lib marl-soccer_amd/lib/exp/lib_$2.so --envs $3 --steps 20 --warmup 5 --every 1 --out $O/stampsd_$2_$3.json > $O/stampsd_$2_$3.log 2>&1 || { tail $O/stampsd_$2_$3.log; return 1; }
+  timeout -k 10 240 python tools/stamps.py --fine --lib marl-soccer_amd/lib/exp/lib_$2.so --envs $3 --steps 20 --warmup 5 --every 1 --out $O/stampsd_$2_$3.json > $O/stampsd_$2_$3.log 2>&1 || { tail $O/stampsd_$2_$3.log; return 1; }
   python -c "import json; d=json.load(open('$O/stampsd_$2_$3.json')); print('$2', $3, 'mean', round(d['wave_cycles_mean']), 'slow5', round(d['wave_cycles_slowest5pct']), 'worst', round(d.get('worst_wave_cycles_mean', 0)), {k: round(v['mean']) for k, v in d['phases'].items()}); t=d['timeline']; print({k: v for k, v in t.items() if k != 'waves_in_phase_per_us_bin'})"
 }
 

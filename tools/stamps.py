@@ -28,6 +28,11 @@ ACC = {16: "AA test", 17: "AA insert", 18: "AA iterations", 19: "SA test", 20: "
 
 # (label, from, to) in kernel order; a stamp inside a branch no lane took is carried forward
 ORDER = [0, 1, 2, 11, 13, 3, 14, 4, 15, 22, 5, 6, 7, 8, 9, 10]
+# --fine (lane-pair kernel): the narrowphase split by pair class (stamps 16-18 instead of the
+# per-lane kernel's accumulators)
+ORDER_FINE = [0, 1, 2, 11, 16, 17, 18, 13, 3, 14, 4, 15, 22, 5, 6, 7, 8, 9, 10]
+LABELS_FINE = {16: "nphase agent-agent", 17: "nphase ball-agent", 18: "nphase static-agent shared tests",
+               13: "nphase static-agent insert"}
 LABELS = {1: "load+actions", 2: "integrate+transforms", 11: "bp+nphase AA/BA", 13: "nphase static-agent",
           3: "nphase ball-wall+cache age", 14: "prestep", 4: "velocity", 15: "warm start",
           22: "solver schedule (lane groups)", 5: "solver x10",
@@ -86,7 +91,12 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--lane-group", type=int, default=None, help="SoccerBatch.set_lane_group(G) (ms_set_lane_group)")
     ap.add_argument("--lib", default=STAMP_LIB, help="a -DMS_STAMPS library (default: the product stamps build)")
+    ap.add_argument("--fine", action="store_true", help="the lane-pair kernel's narrowphase by pair class")
     a, extra = ap.parse_known_args()
+    if a.fine:
+        global ORDER
+        ORDER = ORDER_FINE
+        LABELS.update(LABELS_FINE)
     sys.path.insert(0, PKG)
     if a.build:
         build(extra)
