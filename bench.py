@@ -70,9 +70,10 @@ def parse():
                     help="ms_step kernel (SoccerBatch.set_lane_group): G = 2, 8 or 16 lanes per env, 0 one lane "
                          "per env, -1 automatic; default: the library's (8 lanes while envs x 8 fit the SIMDs, "
                          "else 2)")
-    ap.add_argument("--generic", action="store_true",
-                    help="a non-default reward config (ball_proximity_multiplier 0.003, same physics): times the generic "
-                         "<false> kernels, whose multipliers come from the kernel arguments")
+    ap.add_argument("--generic", choices=("rewards", "physics"), default=None,
+                    help="a non-default config: 'rewards' (ball_proximity_multiplier 0.003) runs the default-physics "
+                         "kernels with runtime reward multipliers (ms_config_specialised 2), 'physics' "
+                         "(action_force_max 150001) the generic kernels with every parameter from the kernel arguments (0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ring-leg", action="store_true", help="skip the frame-ring leg timed beside the headline")
     ap.add_argument("--fused", type=int, default=50, metavar="K",
@@ -133,6 +134,12 @@ def cpu_baseline(args):
                       f"random actions, {cores} threads (every CPU this process may use), {secs:.2f} s wall",
             "single_core": {"value": rate1, "sample": f"{n1} envs x {k1} steps, 1 thread, {secs1:.2f} s"},
             "host": {"cpu_count": os.cpu_count(), "affinity": affinity, "cgroup_cpu_limit": quota, "model": model}}
+
+
+def ring_kernel_name(batch) -> str:
+    """The kernel ms_step_ring launches: the lane-pair frame-ring kernel on the lane-pair launch,
+    else the one-lane one."""
+    return "ms_step_pair_ring_kernel" if batch.lane_group == 2 else "ms_step_ring_kernel"
 
 
 def launch_label(lane_group: int) -> str:
@@ -251,8 +258,10 @@ def main():
         from marlsoccer.config import load_config
         cfg = load_config()
         cfg["simulation"]["max_steps"] = args.max_steps
-        if args.generic:
+        if args.generic == "rewards":
             cfg["rewards"]["ball_proximity_multiplier"] = 0.003
+        elif args.generic == "physics":
+            cfg["physics"]["action_force_max"] = 150001.0
     ring = args.frame_ring
     if ring and args.allgather:
         raise SystemExit("--frame-ring and --allgather are exclusive")
@@ -275,7 +284,7 @@ def main():
 
     launch = (batch.launcher(actions, rew, term, trunc, goal, score) if ring else
               batch.launcher(actions, obs, rew, term, trunc, goal, score))
-    step_kernel = "ms_step_ring_kernel" if ring else batch.step_kernel  # the kernel the timed launches run
+    step_kernel = ring_kernel_name(batch) if ring else batch.step_kernel  # the kernel the timed launches run
 
     nccl = world > 1 and dist.get_backend() == "nccl"
 
@@ -390,12 +399,13 @@ def main():
         r_el = time.perf_counter() - r0
         r_kern = re0.elapsed_time(re1) / args.steps
         rst = rb.stats()
+        r_kernel = ring_kernel_name(rb)
         rb.close()
         r_arb = 0.5 * (rst["cache_entries_read"] + rst["cache_entries_written"]) / max(1, rst["env_steps"])
         r_bytes = RING_BYTES + 2 * 352 / (R - 2) + 2 * ARB_BYTES * r_arb
         r_ach = r_bytes * E / (r_kern * 1e-3) / 1e9
         ring_report = {"value": E * args.steps / r_el, "unit": "env-steps/s", "ms_per_step": r_el * 1e3 / args.steps,
-                       "R": R, "kernel": "ms_step_ring_kernel",
+                       "R": R, "kernel": r_kernel,
                        "roofline": {"bound": "hbm", "achieved": r_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                     "frac": r_ach / HBM_PEAK_GBS, "traffic": None,
                                     "kernel_ms": r_kern, "alg_bytes_per_env_step": r_bytes,
@@ -511,8 +521,9 @@ def main():
             "dtype": "f32",
             "data": f"synthetic: uniform(-1,1) fp32 actions (device Philox, {nsets} distinct (E,4,3) buffers "
                     f"for {args.warmup + args.steps} steps, read from HBM each step); env i seeded 19+i; " +
-                    ("config.json physics, rewards with ball_proximity_multiplier 0.003 (generic kernel)" if args.generic
-                     else "default config.json physics/rewards") + (f", max_steps={args.max_steps}" if args.max_steps != 1000 else ""),
+                    ({"rewards": "config.json physics, ball_proximity_multiplier 0.003 (runtime reward multipliers)",
+                      "physics": "config.json with action_force_max 150001 (generic kernel)"}.get(args.generic,
+                                                                                               "default config.json physics/rewards")) + (f", max_steps={args.max_steps}" if args.max_steps != 1000 else ""),
             "config": {"workload": f"{E} parallel envs per MI355X" +
                                    (" (BASELINE.json configs[2])" if E == 65536 and args.max_steps == 1000 else
                                     " (BASELINE.json configs[1])" if E == 4096 and args.max_steps == 1000 else
@@ -520,7 +531,10 @@ def main():
                                     else ""),
                        "envs_per_gpu": E, "global_envs": world * E, "max_steps": args.max_steps,
                        "parallelism": f"env-shard x{world}" + (" + obs all-gather" if gathered is not None else ""),
-                       "launch": launch_label(batch.lane_group if not ring else 0),
+                       "launch": launch_label(batch.lane_group if not ring or batch.lane_group == 2 else 0),
+                       "specialisation": {1: "default physics and rewards compiled in", 2: "default physics compiled in, "
+                                          "runtime reward multipliers", 0: "generic (every parameter from the kernel "
+                                          "arguments)"}[batch.specialised],
                        **({"obs_layout": f"frame ring, R = {ring} (opt-in; obs is a strided (N, 4, 66) window)"}
                           if ring else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

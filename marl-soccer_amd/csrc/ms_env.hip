@@ -2279,7 +2279,18 @@ int ms_step_ring(ms_env* h, const float* actions, float* frames, int R, int pos,
   (void)rg;
   return fail(MS_ERR_INVALID_ARGUMENT, "ms_step_ring: this experiment build has the lane-pair kernel only");
 #else
-  if (h->default_params)
+  if (h->group == 2) {  // the lane-pair launch (ms_pair.inc), as ms_step takes it
+    const dim3 grid(grid_for(h->n, pr::EPW));
+    if (h->param_mode == 1)
+      hipLaunchKernelGGL(ms_step_pair_ring_kernel<1>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, rg, rew, term,
+                         trunc, goal, score, h->ctr);
+    else if (h->param_mode == 2)
+      hipLaunchKernelGGL(ms_step_pair_ring_kernel<2>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, rg, rew, term,
+                         trunc, goal, score, h->ctr);
+    else
+      hipLaunchKernelGGL(ms_step_pair_ring_kernel<0>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, rg, rew, term,
+                         trunc, goal, score, h->ctr);
+  } else if (h->default_params)
     hipLaunchKernelGGL(ms_step_ring_kernel<true>, dim3(grid_for(h->n, MS_BLOCK)), dim3(MS_BLOCK), 0, h->stream, h->S,
                        h->P, actions, rg, rew, term, trunc, goal, score, h->ctr);
   else

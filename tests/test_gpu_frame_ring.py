@@ -36,10 +36,14 @@ def cfg_dict(**over):
     return c
 
 
-def run_ring_vs_contiguous(ms, n, ring, steps, seed=7, mask_reset_at=None, autoreset=True, **over):
+def run_ring_vs_contiguous(ms, n, ring, steps, seed=7, mask_reset_at=None, autoreset=True, lanes=None, **over):
     config = cfg_dict(**over)
     a = ms.SoccerBatch(n, config=config, autoreset=autoreset)
     b = ms.FrameRingBatch(n, ring=ring, config=config, autoreset=autoreset)
+    if lanes is not None:  # 2: ms_step_ring on the lane-pair launch (ms_step_pair_ring_kernel)
+        a.set_lane_group(lanes)
+        b.set_lane_group(lanes)
+        assert a.lane_group == lanes and b.lane_group == lanes
     oa = a.reset(seed=seed).clone()
     ob = b.reset(seed=seed)
     assert ob.shape == (n, 4, 66) and b.window_index() == 0
@@ -70,19 +74,28 @@ def run_ring_vs_contiguous(ms, n, ring, steps, seed=7, mask_reset_at=None, autor
     return wraps, dones
 
 
+@pytest.mark.parametrize("lanes", [None, 2], ids=["default-launch", "lane-pair"])
 @pytest.mark.parametrize("ring", [4, 6, 32])
-def test_ring_matches_contiguous_with_autoresets(ms, ring):
-    wraps, dones = run_ring_vs_contiguous(ms, 1000, ring, 90, max_steps=20)
+def test_ring_matches_contiguous_with_autoresets(ms, ring, lanes):
+    wraps, dones = run_ring_vs_contiguous(ms, 1000, ring, 90, max_steps=20, lanes=lanes)
     assert wraps >= 2 and dones > 0
 
 
-def test_ring_matches_contiguous_masked_reset_and_manual_reset(ms):
-    run_ring_vs_contiguous(ms, 333, 8, 60, mask_reset_at=23, autoreset=False)
+@pytest.mark.parametrize("lanes", [None, 2], ids=["default-launch", "lane-pair"])
+def test_ring_matches_contiguous_masked_reset_and_manual_reset(ms, lanes):
+    run_ring_vs_contiguous(ms, 333, 8, 60, mask_reset_at=23, autoreset=False, lanes=lanes)
 
 
-def test_ring_generic_kernel_matches_contiguous(ms):
-    # non-default physics: ms_step_ring_kernel<false> (runtime parameters)
-    run_ring_vs_contiguous(ms, 257, 6, 40, max_steps=15, ball_mass=1.5)
+@pytest.mark.parametrize("lanes", [None, 2], ids=["default-launch", "lane-pair"])
+def test_ring_generic_kernel_matches_contiguous(ms, lanes):
+    # non-default physics: the generic kernels (runtime parameters)
+    run_ring_vs_contiguous(ms, 257, 6, 40, max_steps=15, ball_mass=1.5, lanes=lanes)
+
+
+def test_ring_reward_config_lane_pair_matches_contiguous(ms):
+    # reward multipliers only: the lane-pair ring kernel with the default physics compiled in (PM 2)
+    run_ring_vs_contiguous(ms, 300, 8, 60, max_steps=25, score_difference_multiplier=5.0, goal_conceded_penalty=1.0,
+                           lanes=2)
 
 
 def test_ring_full_size_window_matches_contiguous(ms):
@@ -103,9 +116,12 @@ def test_ring_full_size_window_matches_contiguous(ms):
     b.close()
 
 
-def test_ring_window_vs_oracle(ms):
+@pytest.mark.parametrize("lanes", [None, 2], ids=["default-launch", "lane-pair"])
+def test_ring_window_vs_oracle(ms, lanes):
     n, ring, seed = 64, 6, 19
     gpu = ms.FrameRingBatch(n, ring=ring, config=cfg_dict(max_steps=30))
+    if lanes is not None:
+        gpu.set_lane_group(lanes)
     ocfg = orc.MsConfig()
     mc = ms.to_ms_config(cfg_dict(max_steps=30), True)
     for name, _ in mc._fields_:

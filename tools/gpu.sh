@@ -40,6 +40,13 @@ parity() {
   tail -1 $O/pytest.log
 }
 
+ptest() {  # tag test-file: one GPU test file
+  local O=gpurun_out/$1; mkdir -p $O
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu "$2" > $O/pytest_$(basename $2 .py).log 2>&1 \
+    || { tail -40 $O/pytest_$(basename $2 .py).log; return 1; }
+  tail -1 $O/pytest_$(basename $2 .py).log
+}
+
 bench1() {  # tag name bench-args...
   local O=gpurun_out/$1 name=$2; shift 2; mkdir -p $O
   timeout -k 10 300 python bench.py --no-cpu-baseline --no-ring-leg "$@" > $O/bench_$name.json 2> $O/bench_$name.err \
