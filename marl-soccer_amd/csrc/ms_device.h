@@ -602,6 +602,61 @@ __device__ __forceinline__ void unit_mag(float dx, float dy, float* o) {
   o[2] = mag / 1000.0f;  // field diagonal hypot(800, 600)
 }
 
+// unit_mag<true> of two vectors at once, for numerators that are never -0: the lane-pair kernel's fast
+// path requires every position >= +0 (psnap_in_range tests the sign), and each numerator is a position
+// or a positive goal coordinate minus a position, which is -0 only for (-0) - (+0). A +0 numerator
+// leaves the Newton steps at +0 (fma(-d, +0, +0) = +0 for d > 0), so div_nr2's zero selects are not
+// needed. The per-component operations are unit_mag<true>'s, the two vectors' scalar steps (squares,
+// sqrt_nr's residuals, rcp_nr's refinement, the magnitude / 1000) paired as packed fp32.
+__device__ __forceinline__ V2 div_nr2_pos(V2 n, float d, float r) {
+  const V2 nd = V2{-d, -d}, rv = V2{r, r};
+  V2 q = n * rv;
+  V2 e = __builtin_elementwise_fma(nd, q, n);
+  q = __builtin_elementwise_fma(e, rv, q);
+  e = __builtin_elementwise_fma(nd, q, n);
+  return __builtin_elementwise_fma(e, rv, q);
+}
+__device__ __forceinline__ void unit_mag2_pos(float ax, float ay, float bx, float by, float* oa, float* ob) {
+  const V2 X = v2(ax, bx), Y = v2(ay, by);
+  const V2 s2 = X * X + Y * Y;
+  const V2 S = v2(__builtin_amdgcn_sqrtf(s2.x), __builtin_amdgcn_sqrtf(s2.y));
+  const V2 SM = v2(__uint_as_float(__float_as_uint(S.x) - 1u), __uint_as_float(__float_as_uint(S.y) - 1u));
+  const V2 SP = v2(__uint_as_float(__float_as_uint(S.x) + 1u), __uint_as_float(__float_as_uint(S.y) + 1u));
+  const V2 RM = __builtin_elementwise_fma(-SM, S, s2), RP = __builtin_elementwise_fma(-SP, S, s2);
+  V2 M;
+  M.x = RM.x <= 0.0f ? SM.x : S.x;
+  M.x = RP.x > 0.0f ? SP.x : M.x;
+  M.y = RM.y <= 0.0f ? SM.y : S.y;
+  M.y = RP.y > 0.0f ? SP.y : M.y;
+  const V2 R0 = v2(__builtin_amdgcn_rcpf(M.x), __builtin_amdgcn_rcpf(M.y));
+  const V2 E = __builtin_elementwise_fma(-M, R0, V2{1.0f, 1.0f});
+  const V2 R = __builtin_elementwise_fma(E, R0, R0);
+  const bool biga = M.x > 1e-8f, bigb = M.y > 1e-8f;
+  const V2 qa = div_nr2_pos(v2(ax, ay), M.x, R.x), qb = div_nr2_pos(v2(bx, by), M.y, R.y);
+  oa[0] = biga ? qa.x : 0.0f;
+  oa[1] = biga ? qa.y : 0.0f;
+  ob[0] = bigb ? qb.x : 0.0f;
+  ob[1] = bigb ? qb.y : 0.0f;
+  const V2 N = v2(biga ? M.x : 0.0f, bigb ? M.y : 0.0f);  // >= +0: div_nr_nonneg, paired
+  const float r1k = rcp_nr(1000.0f);
+  const V2 qm = div_nr2_pos(N, 1000.0f, r1k);
+  oa[2] = qm.x;
+  ob[2] = qm.y;
+}
+// the same for one vector
+__device__ __forceinline__ void unit_mag_pos(float dx, float dy, float* o) {
+  const V2 d = v2(dx, dy);
+  const V2 d2 = d * d;
+  float mag = sqrt_nr(d2.x + d2.y);
+  const float r = rcp_nr(mag);
+  const bool big = mag > 1e-8f;
+  const V2 q = div_nr2_pos(d, mag, r);
+  o[0] = big ? q.x : 0.0f;
+  o[1] = big ? q.y : 0.0f;
+  mag = big ? mag : 0.0f;
+  o[2] = div_nr_nonneg(mag, 1000.0f, rcp_nr(1000.0f));
+}
+
 // frame of agent i (static), o[22]
 template <int I>
 __device__ __forceinline__ void agent_frame(const Params& P, const float px[5], const float py[5],

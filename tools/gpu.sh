@@ -104,6 +104,19 @@ sq() {  # tag envs bench-args...
   rm -rf $O/p1 $O/p2 $O/p3  # the raw per-dispatch CSVs exceed gpurun's 64-MiB copy-back
 }
 
+vsq() {  # tag envs name...: one SQ pass (instruction mix) over each lib/exp variant's step kernel, steady window
+  local T=$1 N=$2; shift 2
+  local P="SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU"
+  local v
+  for v in "$@"; do
+    local O=gpurun_out/$T/vsq_${v}_$N; mkdir -p $O
+    MARL_SOCCER_LIB=marl-soccer_amd/lib/exp/lib_$v.so timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv -d $O/p1 -o run -- python bench.py --envs $N --warmup 1000 --steps 100 --no-cpu-baseline --no-ring-leg --fused 0 > $O/p1.log 2>&1 \
+      || { echo "vsq $v failed"; tail -5 $O/p1.log; return 1; }
+    echo "--- $v"; python tools/sq_summary.py $O --last 100 --json $O/summary.json | tee $O/summary.txt
+    rm -rf $O/p1
+  done
+}
+
 fused() {  # tag envs K ("+" joins several: 4096+65536 10+50): tools/bench_fused.py sweep, steady window
   local O=gpurun_out/$1; mkdir -p $O
   timeout -k 10 400 python tools/bench_fused.py --envs ${2//+/ } --k ${3//+/ } >> $O/fused.jsonl 2>> $O/fused.err || { tail -5 $O/fused.err; return 1; }
