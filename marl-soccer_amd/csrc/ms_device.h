@@ -162,6 +162,33 @@ __device__ __forceinline__ float div_nr_nonneg(float n, float d, float r) {
   e = __builtin_fmaf(-d, q, n);
   return __builtin_fmaf(e, r, q);
 }
+// One-residual quotients for the frame arithmetic's fixed divisors: 1000 (magnitudes), pi (angle_obs)
+// and the default obs_vmax 200 / obs_wmax 10. For d one of those and r = rcp_nr(d), q0 = n r corrected
+// once, fma(fma(-d, q0, n), r, q0), equals the IEEE n / d for EVERY fp32 numerator of either sign in
+// [2^-100, 2^32) (exhaustive check on the MI355X: tools/div_check.hip, profiles/r05s/div_check.txt),
+// which holds every numerator the fast paths admit; a -0 numerator is kept by the select as in div_nr.
+// obs_div takes this path only where the divisor is one of those constants at compile time (the
+// specialised kernels: ms_config_specialised 1 and 2), div_nr otherwise.
+#ifndef MS_DIV_ONESTEP
+#define MS_DIV_ONESTEP 1
+#endif
+__device__ __forceinline__ float div_k(float n, float d, float r) {
+  const float q = n * r;
+  const float e = __builtin_fmaf(-d, q, n);
+  const float res = __builtin_fmaf(e, r, q);
+  return n == 0.0f ? n : res;
+}
+__device__ __forceinline__ float div_k_nonneg(float n, float d, float r) {  // n never -0
+  const float q = n * r;
+  return __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+}
+__device__ __forceinline__ bool div_k_ok(float d) {
+  return MS_DIV_ONESTEP && __builtin_constant_p(d) && (d == 200.0f || d == 10.0f || d == 1000.0f);
+}
+__device__ __forceinline__ float obs_div(float n, float d) {
+  if (div_k_ok(d)) return div_k(n, d, rcp_nr(d));
+  return div_nr(n, d, rcp_nr(d));
+}
 __device__ __forceinline__ float sqrt_nr(float x) {
   float s = __builtin_amdgcn_sqrtf(x);
   const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
@@ -175,7 +202,10 @@ template <bool FAST = false>
 __device__ __forceinline__ float angle_obs(float a) {
   float k = rintf(a * 0.15915493667125702f);
   float w = (a - k * 6.28125f) - k * 0.0019353071693331003f;
-  if constexpr (FAST) return div_nr(w, 3.1415927410125732f, rcp_nr(3.1415927410125732f));
+  if constexpr (FAST) {
+    if (MS_DIV_ONESTEP) return div_k(w, 3.1415927410125732f, rcp_nr(3.1415927410125732f));
+    return div_nr(w, 3.1415927410125732f, rcp_nr(3.1415927410125732f));
+  }
   return w / 3.1415927410125732f;
 }
 
@@ -587,7 +617,7 @@ __device__ __forceinline__ void unit_mag(float dx, float dy, float* o) {
     o[0] = big ? q.x : 0.0f;
     o[1] = big ? q.y : 0.0f;
     mag = big ? mag : 0.0f;
-    o[2] = div_nr_nonneg(mag, 1000.0f, rcp_nr(1000.0f));  // mag >= +0
+    o[2] = MS_DIV_ONESTEP ? div_k_nonneg(mag, 1000.0f, rcp_nr(1000.0f)) : div_nr_nonneg(mag, 1000.0f, rcp_nr(1000.0f));  // mag >= +0
     return;
   }
   float mag = sqrtf(dx * dx + dy * dy);
@@ -639,7 +669,13 @@ __device__ __forceinline__ void unit_mag2_pos(float ax, float ay, float bx, floa
   ob[1] = bigb ? qb.y : 0.0f;
   const V2 N = v2(biga ? M.x : 0.0f, bigb ? M.y : 0.0f);  // >= +0: div_nr_nonneg, paired
   const float r1k = rcp_nr(1000.0f);
-  const V2 qm = div_nr2_pos(N, 1000.0f, r1k);
+  V2 qm;
+  if (MS_DIV_ONESTEP) {
+    const V2 q = N * V2{r1k, r1k};
+    qm = __builtin_elementwise_fma(__builtin_elementwise_fma(V2{-1000.0f, -1000.0f}, q, N), V2{r1k, r1k}, q);
+  } else {
+    qm = div_nr2_pos(N, 1000.0f, r1k);
+  }
   oa[2] = qm.x;
   ob[2] = qm.y;
 }
@@ -654,7 +690,7 @@ __device__ __forceinline__ void unit_mag_pos(float dx, float dy, float* o) {
   o[0] = big ? q.x : 0.0f;
   o[1] = big ? q.y : 0.0f;
   mag = big ? mag : 0.0f;
-  o[2] = div_nr_nonneg(mag, 1000.0f, rcp_nr(1000.0f));
+  o[2] = MS_DIV_ONESTEP ? div_k_nonneg(mag, 1000.0f, rcp_nr(1000.0f)) : div_nr_nonneg(mag, 1000.0f, rcp_nr(1000.0f));
 }
 
 // frame of agent i (static), o[22]

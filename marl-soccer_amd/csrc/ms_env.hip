@@ -336,9 +336,9 @@ __device__ __forceinline__ void agent_frame_store(const Params& P, const Snap& s
   constexpr int OTH[3] = {TEAM, O1, O2};
   float f[22];
   if constexpr (FAST) {
-    f[0] = div_nr(s.vx[A], P.obs_vmax, rcp_nr(P.obs_vmax));
-    f[1] = div_nr(s.vy[A], P.obs_vmax, rcp_nr(P.obs_vmax));
-    f[3] = div_nr(s.w[A], P.obs_wmax, rcp_nr(P.obs_wmax));
+    f[0] = obs_div(s.vx[A], P.obs_vmax);
+    f[1] = obs_div(s.vy[A], P.obs_vmax);
+    f[3] = obs_div(s.w[A], P.obs_wmax);
   } else {
     f[0] = s.vx[A] / P.obs_vmax;
     f[1] = s.vy[A] / P.obs_vmax;
@@ -504,9 +504,9 @@ __device__ __forceinline__ void frame_store_at(const Params& P, const Snap& s, c
   constexpr int OTH[3] = {TEAM, O1, O2};
   float f[22];
   if constexpr (FAST) {
-    f[0] = div_nr(s.vx[A], P.obs_vmax, rcp_nr(P.obs_vmax));
-    f[1] = div_nr(s.vy[A], P.obs_vmax, rcp_nr(P.obs_vmax));
-    f[3] = div_nr(s.w[A], P.obs_wmax, rcp_nr(P.obs_wmax));
+    f[0] = obs_div(s.vx[A], P.obs_vmax);
+    f[1] = obs_div(s.vy[A], P.obs_vmax);
+    f[3] = obs_div(s.w[A], P.obs_wmax);
   } else {
     f[0] = s.vx[A] / P.obs_vmax;
     f[1] = s.vy[A] / P.obs_vmax;
