@@ -326,9 +326,9 @@ def main():
             gather_into(gathered)
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if world > 1:  # (one rank: nothing runs between the two, so the first synchronize closes the window)
         dist.barrier()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     # the arbiter-cache entries the timed launches read and wrote (counted by the kernel)
