@@ -39,6 +39,15 @@ __global__ void check(float d, uint32_t lo, uint32_t hi, unsigned long long* bad
   }
 }
 
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                  \
+      return 2;                                                                \
+    }                                                                          \
+  } while (0)
+
 int main() {
   struct Case { const char* name; float d; uint32_t lo, hi; };
   const Case cases[] = {
@@ -55,17 +64,19 @@ int main() {
   };
   unsigned long long* bad;
   uint32_t* first;
-  hipMalloc(&bad, sizeof(unsigned long long));
-  hipMalloc(&first, 4 * sizeof(uint32_t));
+  CK(hipMalloc(&bad, sizeof(unsigned long long)));
+  CK(hipMalloc(&first, 4 * sizeof(uint32_t)));
   int fails = 0;
   for (const Case& c : cases) {
-    hipMemset(bad, 0, sizeof(unsigned long long));
-    hipMemset(first, 0, 4 * sizeof(uint32_t));
+    CK(hipMemset(bad, 0, sizeof(unsigned long long)));
+    CK(hipMemset(first, 0, 4 * sizeof(uint32_t)));
     hipLaunchKernelGGL(check, dim3(8192), dim3(256), 0, 0, c.d, c.lo, c.hi, bad, first);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
     unsigned long long nb = 0;
     uint32_t f[4];
-    hipMemcpy(&nb, bad, sizeof(nb), hipMemcpyDeviceToHost);
-    hipMemcpy(f, first, sizeof(f), hipMemcpyDeviceToHost);
+    CK(hipMemcpy(&nb, bad, sizeof(nb), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(f, first, sizeof(f), hipMemcpyDeviceToHost));
     printf("%-22s d=%a numerators [%08x, %08x] x 2 signs: %llu mismatches", c.name, c.d, c.lo, c.hi, nb);
     for (int k = 0; k < 4 && k < (int)nb; ++k) {
       float v;
@@ -75,7 +86,7 @@ int main() {
     printf("\n");
     fails += nb != 0;
   }
-  hipFree(bad);
-  hipFree(first);
+  CK(hipFree(bad));
+  CK(hipFree(first));
   return fails ? 1 : 0;
 }
