@@ -49,18 +49,18 @@ __global__ void check(float d, uint32_t lo, uint32_t hi, unsigned long long* bad
   } while (0)
 
 int main() {
-  struct Case { const char* name; float d; uint32_t lo, hi; };
+  struct Case { const char* name; float d; uint32_t lo, hi; bool domain; };
   const Case cases[] = {
       // the fast path's numerator domain: 2^-100 .. 2^32 (frame_inputs_in_range / psnap_in_range)
-      {"mag / 1000", 1000.0f, 0x0D800000u, 0x4F800000u},
-      {"v / 200 (obs_vmax)", 200.0f, 0x0D800000u, 0x4F800000u},
-      {"w / 10 (obs_wmax)", 10.0f, 0x0D800000u, 0x4F800000u},
-      {"angle / pi", 3.1415927410125732f, 0x0D800000u, 0x40800000u},  // .. 4
+      {"mag / 1000", 1000.0f, 0x0D800000u, 0x4F800000u, true},
+      {"v / 200 (obs_vmax)", 200.0f, 0x0D800000u, 0x4F800000u, true},
+      {"w / 10 (obs_wmax)", 10.0f, 0x0D800000u, 0x4F800000u, true},
+      {"angle / pi", 3.1415927410125732f, 0x0D800000u, 0x40800000u, true},  // .. 4
       // every normal numerator (information: where the shorter sequence stops agreeing)
-      {"mag / 1000 (normals)", 1000.0f, 0x00800000u, 0x7F000000u},
-      {"v / 200 (normals)", 200.0f, 0x00800000u, 0x7F000000u},
-      {"w / 10 (normals)", 10.0f, 0x00800000u, 0x7F000000u},
-      {"angle / pi (normals)", 3.1415927410125732f, 0x00800000u, 0x7F000000u},
+      {"mag / 1000 (normals)", 1000.0f, 0x00800000u, 0x7F000000u, false},
+      {"v / 200 (normals)", 200.0f, 0x00800000u, 0x7F000000u, false},
+      {"w / 10 (normals)", 10.0f, 0x00800000u, 0x7F000000u, false},
+      {"angle / pi (normals)", 3.1415927410125732f, 0x00800000u, 0x7F000000u, false},
   };
   unsigned long long* bad;
   uint32_t* first;
@@ -84,7 +84,7 @@ int main() {
       printf(" %08x(%a)", f[k], v);
     }
     printf("\n");
-    fails += nb != 0;
+    fails += c.domain && nb != 0;  // (the rows over every normal numerator are information)
   }
   CK(hipFree(bad));
   CK(hipFree(first));
