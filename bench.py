@@ -318,8 +318,8 @@ def main():
     # profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace) gives the exact one.
     stream = batch.stream
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)  # (a marker on the idle stream: the wall clock starts at the first launch)
     t0 = time.perf_counter()
-    ev0.record(stream)
     for i in range(args.steps):
         launch(args.warmup + i)
         if gathered is not None:
