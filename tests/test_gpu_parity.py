@@ -623,3 +623,56 @@ def test_lane_pair_full_size_equals_per_lane(ms, n, max_steps, steps):
     assert sb["arbiter_overflow"] == 0
     a.close()
     b.close()
+
+
+def test_kernel_switching_between_steps_bitexact(ms):
+    """The step kernels leave one state format, so a batch may change kernels between steps: lane
+    pairs, lane groups (8, 16), one lane per env, and the K-step launch, in an irregular order, with
+    chase actions, goals and auto-resets (max_steps 40). The lane-pair kernel carries its fast-path
+    range decisions of the t-1 / t-2 snapshots in the history pad (MS_PAIR_RANGE_CACHE); every other
+    kernel stores +0 there, so after a switch the pair kernel takes the IEEE frame path until its own
+    decisions are in place. Obs and rewards at every step and the whole state at the end against the
+    fp32 oracle."""
+    n = 320
+    cfg = cfg_dict(max_steps=40)
+    gpu = ms.SoccerBatch(n, config=cfg)
+    ref = orc.OracleBatch(n, "f32", oracle_cfg(gpu._cfg))
+    pcg = np.stack([orc.pcg_from_seed(41 + i) for i in range(n)])
+    gpu.reset(seed=41)
+    ref.reset(pcg, 0)
+    rng = np.random.default_rng(41)
+    chaser = np.arange(n) % 4
+    plan = [2, 2, 2, 8, 2, 2, 0, 2, 2, 2, "n3", 2, 2, 16, 2, 8, 8, 2, 2, 2, "n2", 0, 2, 2, 2] * 4
+    t = 0
+    for what in plan:
+        if isinstance(what, str):  # a K-step launch (lane pairs)
+            K = int(what[1:])
+            gpu.set_lane_group(2)
+            acts, want = [], []
+            for _ in range(K):
+                st = ref.export_state()
+                pos = np.stack([st["body"]["px"], st["body"]["py"]], -1)
+                act = sh.chase_actions(pos, st["body"]["angle"][:, :4], rng, chaser)
+                obs, rew, trunc, goal, score, bad = ref.step(act)
+                assert bad == 0
+                acts.append(act)
+                want.append((obs, rew))
+            out = gpu.step_n(torch.from_numpy(np.stack(acts)).to(gpu.device))
+            for k, (obs, rew) in enumerate(want):
+                np.testing.assert_array_equal(out.obs[k].cpu().numpy(), obs, err_msg=f"step_n obs t={t + k}")
+                np.testing.assert_array_equal(out.rew[k].cpu().numpy(), rew.astype(np.float32),
+                                              err_msg=f"step_n rew t={t + k}")
+            t += K
+            continue
+        gpu.set_lane_group(what)
+        st = ref.export_state()
+        pos = np.stack([st["body"]["px"], st["body"]["py"]], -1)
+        act = sh.chase_actions(pos, st["body"]["angle"][:, :4], rng, chaser)
+        o = gpu.step(torch.from_numpy(act).to(gpu.device))
+        obs, rew, trunc, goal, score, bad = ref.step(act)
+        assert bad == 0
+        np.testing.assert_array_equal(o.obs.cpu().numpy(), obs, err_msg=f"obs t={t} lanes={what}")
+        np.testing.assert_array_equal(o.rew.cpu().numpy(), rew.astype(np.float32), err_msg=f"rew t={t} lanes={what}")
+        t += 1
+    assert_state_equal(gpu.export_state(), ref.export_state(), "end")
+    gpu.close()
