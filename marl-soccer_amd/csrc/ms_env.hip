@@ -2144,15 +2144,15 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
     return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: misaligned buffer (actions/rew 16 B, obs/score 8 B, flags 4 B)");
   [[maybe_unused]] const unsigned nblk = grid_for(h->n, MS_BLOCK);
   if (h->group == 2) {
-    const dim3 grid(grid_for(h->n, pr::EPW));
+    const dim3 grid(grid_for(h->n, pr::EPW * MS_PAIR_WG)), blk(64 * MS_PAIR_WG);
     if (h->param_mode == 1)
-      hipLaunchKernelGGL(ms_step_pair_kernel<1>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew, term,
+      hipLaunchKernelGGL(ms_step_pair_kernel<1>, grid, blk, 0, h->stream, h->S, h->P, actions, obs, rew, term,
                          trunc, goal, score, h->ctr);
     else if (h->param_mode == 2)
-      hipLaunchKernelGGL(ms_step_pair_kernel<2>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew, term,
+      hipLaunchKernelGGL(ms_step_pair_kernel<2>, grid, blk, 0, h->stream, h->S, h->P, actions, obs, rew, term,
                          trunc, goal, score, h->ctr);
     else
-      hipLaunchKernelGGL(ms_step_pair_kernel<0>, grid, dim3(64), 0, h->stream, h->S, h->P, actions, obs, rew,
+      hipLaunchKernelGGL(ms_step_pair_kernel<0>, grid, blk, 0, h->stream, h->S, h->P, actions, obs, rew,
                          term, trunc, goal, score, h->ctr);
   } else {
 #ifdef MS_PAIR_ONLY  // experiment builds (tools/variants.py): the lane-pair kernels only
