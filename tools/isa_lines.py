@@ -102,10 +102,8 @@ def main():
     by_func = collections.defaultdict(collections.Counter)
     by_line = collections.defaultdict(collections.Counter)
     total = collections.Counter()
-    labels = {}
-    for i, (kind, op, loc) in enumerate(body):
+    for kind, op, loc in body:
         if kind == "label":
-            labels[op] = i
             continue
         k = klass(op)
         base, fn, line = where(loc)
@@ -117,11 +115,7 @@ def main():
     for (base, fn), c in sorted(by_func.items(), key=lambda kv: -kv[1]["valu"])[: args.top]:
         print(f"  {c['valu']:6d} {c['lds']:5d} {c['vmem']:5d} {c['salu']:5d}  {base}:{fn}")
     # loops: a branch to an earlier label
-    print("\nloops (backward branches): body span, static VALU inside, source lines of the branch")
-    for i, (kind, op, loc) in enumerate(body):
-        if kind != "inst" or not op.startswith("s_cbranch") and op != "s_branch":
-            continue
-    pos = 0
+    print("\nloops (backward branches): body span, static VALU inside, source functions of the body")
     with open(asm) as f:
         text = f.read()
     start = text.index(name + ":")
@@ -143,8 +137,6 @@ def main():
         c = collections.Counter(klass(x[1]) for x in insts[a:b + 1])
         fns = collections.Counter(where(x[2])[1] for x in insts[a:b + 1])
         print(f"  [{a:6d},{b:6d}] valu {c['valu']:5d} lds {c['lds']:4d} vmem {c['vmem']:3d}  {', '.join(f'{k}:{v}' for k, v in fns.most_common(4))}")
-    if args.top and False:
-        pass
 
 
 if __name__ == "__main__":
