@@ -22,7 +22,7 @@ SOURCES = [os.path.join(CSRC, "ms_env.hip"), os.path.join(CSRC, "ms_policy.hip")
 # per-source flags: the K-step kernels (ms_kstep.hip) without LLVM's machine loop-invariant code motion,
 # which hoisted per-step values out of their K-step loop and spilled them
 UNIT_FLAGS = {"ms_kstep.hip": ["-mllvm", "-disable-machine-licm"]}
-DEPS = SOURCES + [os.path.join(CSRC, "ms_device.h"), os.path.join(CSRC, "ms_group.inc"), os.path.join(CSRC, "ms_pair.inc"), os.path.join(ROOT, "include", "marl_soccer.h")]
+DEPS = SOURCES + [os.path.join(CSRC, "ms_device.h"), os.path.join(CSRC, "ms_diag.h"), os.path.join(CSRC, "ms_group.inc"), os.path.join(CSRC, "ms_pair.inc"), os.path.join(ROOT, "include", "marl_soccer.h")]
 ARCH = os.environ.get("MS_OFFLOAD_ARCH", "gfx950")
 # LLVM's default AMDGPU machine scheduler. The max-ILP strategy (-mllvm
 # -amdgpu-sched-strategy=max-ilp, -2.6 % step time in round 1) produced kernels that fault on the

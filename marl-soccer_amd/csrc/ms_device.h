@@ -648,11 +648,6 @@ __device__ __forceinline__ V2 div_nr2_pos(V2 n, float d, float r) {
 }
 __device__ __forceinline__ void unit_mag_pos(float dx, float dy, float* o);
 __device__ __forceinline__ void unit_mag2_pos(float ax, float ay, float bx, float by, float* oa, float* ob) {
-#ifdef MS_UMAG2_SCALAR  // (A/B: one after the other, no packing: +25 static VALU in the pair kernel)
-  unit_mag_pos(ax, ay, oa);
-  unit_mag_pos(bx, by, ob);
-  return;
-#endif
   const V2 X = v2(ax, bx), Y = v2(ay, by);
   const V2 s2 = X * X + Y * Y;
   const V2 S = v2(__builtin_amdgcn_sqrtf(s2.x), __builtin_amdgcn_sqrtf(s2.y));

@@ -105,43 +105,7 @@ struct Counters {
 };
 
 
-#ifdef MS_STAMPS
-// slot k: s_memtime (shader cycles; its counter is per XCD, so cross-wave comparisons hold within
-// an XCD only); slot 24 + k: s_memrealtime (the 100-MHz clock every XCD shares: the launch timeline)
-#define STAMP(k)                                                                         \
-  do {                                                                                   \
-    unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
-    unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                            \
-    const unsigned long long act_ = __ballot(1);                                          \
-    if ((int)(threadIdx.x & 63) == __ffsll((long long)act_) - 1 && S.stamps) {            \
-      S.stamps[stamp_row * MS_NSTAMP + (k)] = t_;                                        \
-      S.stamps[stamp_row * MS_NSTAMP + 24 + (k)] = r_;                                   \
-    }                                                                                    \
-  } while (0)
-// cycles spent inside a region of a divergent loop, accumulated per lane; the wave's figure is
-// the maximum over its lanes (the lane that ran the most iterations), written to slot k
-#define ACC_DECL(v) unsigned long long v = 0
-#define ACC_BEGIN(v) const unsigned long long v##_t0 = __builtin_amdgcn_s_memtime()
-#define ACC_END(v) v += __builtin_amdgcn_s_memtime() - v##_t0
-#define ACC_INC(v) v++
-#define ACC_STORE(v, k)                                                                    \
-  do {                                                                                   \
-    unsigned long long m_ = v;                                                           \
-    for (int o_ = 32; o_ > 0; o_ >>= 1) {                                                \
-      const unsigned long long x_ = __shfl_xor(m_, o_);                                  \
-      m_ = x_ > m_ ? x_ : m_;                                                            \
-    }                                                                                    \
-    if ((threadIdx.x & 63) == 0 && S.stamps) S.stamps[stamp_row * MS_NSTAMP + (k)] = m_;       \
-  } while (0)
-#else
-#define STAMP(k) do { } while (0)
-#define ACC_DECL(v) do { } while (0)
-#define ACC_BEGIN(v) do { } while (0)
-#define ACC_END(v) do { } while (0)
-#define ACC_INC(v) do { } while (0)
-#define ACC_STORE(v, k) do { } while (0)
-#endif
-#define MS_NSTAMP 48  // [0, 24): cycles and accumulators; [24, 48): real time of stamps 0..23
+#include "ms_diag.h"  // STAMP / ACC_* phase stamps (empty unless -DMS_STAMPS)
 
 // ---- per-lane env register file ------------------------------------------------------------
 struct Env {
@@ -2144,7 +2108,7 @@ int ms_step(ms_env* h, const float* actions, float* obs, float* rew, uint8_t* te
     return fail(MS_ERR_INVALID_ARGUMENT, "ms_step: misaligned buffer (actions/rew 16 B, obs/score 8 B, flags 4 B)");
   [[maybe_unused]] const unsigned nblk = grid_for(h->n, MS_BLOCK);
   if (h->group == 2) {
-    const dim3 grid(grid_for(h->n, pr::EPW * MS_PAIR_WG)), blk(64 * MS_PAIR_WG);
+    const dim3 grid(grid_for(h->n, pr::EPW)), blk(64);
     if (h->param_mode == 1)
       hipLaunchKernelGGL(ms_step_pair_kernel<1>, grid, blk, 0, h->stream, h->S, h->P, actions, obs, rew, term,
                          trunc, goal, score, h->ctr);

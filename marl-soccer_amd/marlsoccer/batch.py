@@ -221,7 +221,10 @@ class SoccerBatch:
         steps are one launch. An env-step skipped for a non-finite action writes step()'s defined
         values into its slot (NaN obs and rewards, term / trunc / goal 0, the current score);
         check=True synchronises and raises the reference's ValueError for the first such env, as
-        step(check=True) does."""
+        step(check=True) does. The check covers every env-step since the last check (or
+        reset_stats()), as raise_if_nonfinite does: a non-finite action handed to an earlier
+        unchecked step() / step_n() raises here too, and the message then says that the action
+        was not in this call's tensor."""
         if actions.dim() != 4 or actions.shape[1:] != (self.num_envs, 4, 3):
             raise ValueError(f"actions must have shape (K, {self.num_envs}, 4, 3), got {tuple(actions.shape)}")
         K = int(actions.shape[0])
@@ -252,7 +255,11 @@ class SoccerBatch:
             if st["nonfinite_envs"]:
                 e = st["first_nonfinite_env"]
                 bad = (~torch.isfinite(actions[:, e]).all(dim=-1)).any(dim=-1).nonzero()
-                self.raise_if_nonfinite(actions[int(bad[0, 0])] if bad.numel() else None)
+                if bad.numel():
+                    self.raise_if_nonfinite(actions[int(bad[0, 0])])
+                self.reset_stats()
+                raise ValueError(f"Action contains non-finite values (env {e}, in an earlier unchecked step, "
+                                 f"not in this step_n call's actions; {st['nonfinite_envs']} env-step(s) not stepped)")
         return StepOutput((o["obs"], o["rew"], o["term"], o["trunc"], o["goal"], o["score"]))
 
     def raise_if_nonfinite(self, actions: torch.Tensor | None = None) -> None:
@@ -420,8 +427,9 @@ class FrameRingBatch(SoccerBatch):
     R - 2 steps the window moves back to the ring's start and that step writes all three
     frames. An env not stepped because of a non-finite action writes no frame, and the window
     still advances: its window holds a stale frame (zeros or one from R - 2 steps back) until two
-    more valid steps have pushed it out, whereas SoccerBatch's contiguous obs keeps the previous
-    observation. Both raise via raise_if_nonfinite; after catching that ValueError, call
+    more valid steps have pushed it out, whereas SoccerBatch's contiguous step writes defined
+    values for such an env (ABI 5: an all-NaN obs row, NaN rewards, term / trunc / goal 0 and the
+    current score). Both raise via raise_if_nonfinite; after catching that ValueError, call
     reset(mask=...) for that env before reading its window again.
     """
 

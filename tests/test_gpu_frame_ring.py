@@ -87,6 +87,15 @@ def test_ring_matches_contiguous_masked_reset_and_manual_reset(ms, lanes):
 
 
 @pytest.mark.parametrize("lanes", [None, 2], ids=["default-launch", "lane-pair"])
+def test_ring_matches_contiguous_staggered_episode_clocks(ms, lanes):
+    # a masked reset with auto-reset on: the masked envs' episodes end 7 steps after the others', so
+    # on steps where the window does not wrap a wave holds refilling and shifting envs at once (the
+    # lane-pair ring kernel's three-frame path must then keep the shifting envs' frame t-2)
+    wraps, dones = run_ring_vs_contiguous(ms, 1000, 32, 70, mask_reset_at=7, max_steps=20, lanes=lanes)
+    assert dones > 0
+
+
+@pytest.mark.parametrize("lanes", [None, 2], ids=["default-launch", "lane-pair"])
 def test_ring_generic_kernel_matches_contiguous(ms, lanes):
     # non-default physics: the generic kernels (runtime parameters)
     run_ring_vs_contiguous(ms, 257, 6, 40, max_steps=15, ball_mass=1.5, lanes=lanes)

@@ -322,9 +322,10 @@ def test_config_sizes_hash_actions_subsample(ms, n, max_steps, steps, env0):
     auto-reset, config 3's rank-3 shard (65,536 envs / 8 GPUs = 8,192, global envs
     24,576..32,767) for 120 steps, config 4's rank-5 shard (262,144 / 8 = 32,768, max_steps=512)
     over a whole episode plus its auto-reset). A shard is seeded and driven by its global env
-    indices (seed 19 + g), as bench.py and marlsoccer.distributed do. Every 20th step the obs of
-    a 64-env subsample match the fp32 oracle bit for bit; at the end state is finite and inside
-    the field, no arbiter overflowed. (Device-Philox uniform actions as in the bench:
+    indices (seed 19 + g), as bench.py and marlsoccer.distributed do. At every step the rewards,
+    truncation flags, goal flags and scores of a 64-env subsample match the fp32 oracle bit for bit,
+    and every 20th step their obs; at the end the subsample's state equals the oracle's, the whole
+    batch's is finite and inside the field, no arbiter overflowed. (Device-Philox uniform actions as in the bench:
     test_config5_whole_batch_one_gpu_subsample.)"""
     gpu = ms.SoccerBatch(n, config=cfg_dict(max_steps=max_steps))
     gpu.reset(seed=19 + env0)
@@ -336,12 +337,20 @@ def test_config_sizes_hash_actions_subsample(ms, n, max_steps, steps, env0):
     for t in range(steps):
         act = sh.hash_actions(n, t, env0=env0)
         out = gpu.step(torch.from_numpy(act).to(gpu.device))
-        robs, _, rtrunc = ref.step(act[sub])[:3]
+        robs, rrew, rtrunc, rgoal, rscore = ref.step(act[sub])[:5]
         dones += int(rtrunc[:, 0].sum())
+        np.testing.assert_array_equal(out.rew[sub_d].cpu().numpy(), rrew.astype(np.float32), err_msg=f"rew t={t}")
+        np.testing.assert_array_equal(out.trunc[sub_d].cpu().numpy().astype(bool), rtrunc, err_msg=f"trunc t={t}")
+        np.testing.assert_array_equal(out.goal[sub_d].cpu().numpy(), rgoal, err_msg=f"goal t={t}")
+        np.testing.assert_array_equal(out.score[sub_d].cpu().numpy(), rscore, err_msg=f"score t={t}")
         if t % 20 == 19 or t == max_steps - 1:
             np.testing.assert_array_equal(out.obs[sub_d].cpu().numpy(), robs, err_msg=f"t={t}")
     assert dones == 64 * (steps // max_steps)
     st = gpu.export_state()
+    r = ref.export_state()
+    for f in ("px", "py", "vx", "vy", "angle", "w"):
+        np.testing.assert_array_equal(st["body"][f][sub], r["body"][f], err_msg=f"body.{f}")
+    np.testing.assert_array_equal(st["steps"][sub], r["steps"])
     assert np.isfinite(st["body"]["px"]).all() and np.isfinite(st["body"]["vx"]).all()
     assert (st["body"]["px"] > -50).all() and (st["body"]["px"] < 850).all()
     assert (st["body"]["py"] > -50).all() and (st["body"]["py"] < 650).all()
@@ -353,7 +362,8 @@ def test_config5_whole_batch_one_gpu_subsample(ms):
     """BASELINE config 5's whole batch on one GPU: 262,144 envs, max_steps=512, a whole episode
     plus its auto-reset (560 steps). Actions are uniform(-1, 1) from the device Philox (as in the
     bench); the 64-env subsample's rows are copied to the host and stepped through the fp32
-    oracle, whose obs, rewards and final state must match the GPU's bit for bit."""
+    oracle, whose rewards, flags and scores (every step), obs (every 20th step) and final state
+    must match the GPU's bit for bit."""
     n, max_steps, steps = 262144, 512, 560
     gpu = ms.SoccerBatch(n, config=cfg_dict(max_steps=max_steps))
     gpu.reset(seed=19)
@@ -367,11 +377,14 @@ def test_config5_whole_batch_one_gpu_subsample(ms):
     for t in range(steps):
         act = torch.rand((n, 4, 3), generator=gen, device=gpu.device) * 2.0 - 1.0
         out = gpu.step(act)
-        robs, rrew, rtrunc = ref.step(act[sub_d].cpu().numpy())[:3]
+        robs, rrew, rtrunc, rgoal, rscore = ref.step(act[sub_d].cpu().numpy())[:5]
         dones += int(rtrunc[:, 0].sum())
+        np.testing.assert_array_equal(out.rew[sub_d].cpu().numpy(), rrew.astype(np.float32), err_msg=f"rew t={t}")
+        np.testing.assert_array_equal(out.trunc[sub_d].cpu().numpy().astype(bool), rtrunc, err_msg=f"trunc t={t}")
+        np.testing.assert_array_equal(out.goal[sub_d].cpu().numpy(), rgoal, err_msg=f"goal t={t}")
+        np.testing.assert_array_equal(out.score[sub_d].cpu().numpy(), rscore, err_msg=f"score t={t}")
         if t % 20 == 19 or t == max_steps - 1:
             np.testing.assert_array_equal(out.obs[sub_d].cpu().numpy(), robs, err_msg=f"obs t={t}")
-            np.testing.assert_array_equal(out.rew[sub_d].cpu().numpy(), rrew.astype(np.float32), err_msg=f"rew t={t}")
     assert dones == 64  # every subsampled env crossed its episode end and auto-reset
     g = gpu.export_state()
     r = ref.export_state()
