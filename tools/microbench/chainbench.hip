@@ -77,6 +77,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         });
       }
     }
+  } else if (MODE == 3 || MODE == 4) {
+    // solve_h with the read quads held to the end (no write-after-write wait on their 4th register);
+    // MODE 4: the two record byte addresses precomputed per slot (one packed word)
+    uint32_t ad[NC];
+    static_for<0, NC>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      const uint32_t base = (uint32_t)((char*)rec - (char*)&L);
+      ad[k] = (base + CS_BA(reg[k].m) * 512u) | ((base + CS_BB(reg[k].m) * 512u) << 16);
+    });
+    for (int rep = 0; rep < reps; ++rep) {
+#pragma unroll 1
+      for (int it = 0; it < 10; ++it) {
+        static_for<0, NC>([&](auto kc) __attribute__((always_inline)) {
+          constexpr int k = decltype(kc)::value;
+          asm volatile("" : "+v"(reg[k].m), "+v"(ad[k]));
+          HSlot& c = reg[k];
+          const int ba = CS_BA(c.m), bb = CS_BB(c.m);
+          float4* pa;
+          float4* pb;
+          if (MODE == 4) {
+            pa = (float4*)((char*)&L + (ad[k] & 0xffffu));
+            pb = (float4*)((char*)&L + (ad[k] >> 16));
+          } else {
+            pa = rec + ba * 32;
+            pb = rec + bb * 32;
+          }
+          const F4 qa = lds_f4(pa), qb = lds_f4(pb);
+          const float2 A = L.mass[ba], B = L.mass[bb];
+          V2 xa, xb;
+          float xwa, xwb;
+          solve_h_core(c, A.x, A.y, B.x, B.y, v2(qa.x, qa.y), qa.z, v2(qb.x, qb.y), qb.z, xa, xwa, xb, xwb);
+          float* da = (float*)pa;
+          da[0] = xa.x; da[1] = xa.y; da[2] = xwa;
+          float* db = (float*)pb;
+          db[0] = xb.x; db[1] = xb.y; db[2] = xwb;
+          asm volatile("" ::"v"(qa), "v"(qb));
+        });
+      }
+    }
   } else {
     // the first contact's inputs
     V2 va, vb;
@@ -109,9 +148,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           // the next contact's records as they stand before this contact's writes
           V2 pa, pb;
           float pwa, pwb;
+          F4 pqa = F4{0.f, 0.f, 0.f, 0.f}, pqb = pqa;
           if (MODE == 1) {
-            const F4 qa = lds_f4(rec + na_ * 32), qb = lds_f4(rec + nb_ * 32);
-            pa = v2(qa.x, qa.y); pwa = qa.z; pb = v2(qb.x, qb.y); pwb = qb.z;
+            pqa = lds_f4(rec + na_ * 32);
+            pqb = lds_f4(rec + nb_ * 32);
+            pa = v2(pqa.x, pqa.y); pwa = pqa.z; pb = v2(pqb.x, pqb.y); pwb = pqb.z;
+            __builtin_amdgcn_sched_barrier(0);  // the reads issue before this contact's chain
           } else {
             pa = v2(0.f, 0.f); pb = pa; pwa = 0.f; pwb = 0.f;
 #pragma unroll
@@ -140,6 +182,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           wa = na_ == ba ? xwa : (na_ == bb ? xwb : pwa);
           vb = nb_ == ba ? xa : (nb_ == bb ? xb : pb);
           wb = nb_ == ba ? xwa : (nb_ == bb ? xwb : pwb);
+          // (MODE 1) the early reads' whole destination quads stay allocated until here: reusing their
+          // unused 4th register as a temporary makes the chain wait for the read (write-after-write)
+          if (MODE == 1) asm volatile("" ::"v"(pqa), "v"(pqb));
         });
       }
     }
@@ -185,6 +230,14 @@ int main() {
   std::vector<float> h0(64 * GMAX), h1(64 * GMAX), h2(64 * GMAX);
   for (int grid : {1, 2048}) {
     for (int r = 0; r < 2; ++r) {
+      {
+        double c3 = run<3, 0>(cyc, out, grid, reps, h1.data());
+        double c4 = run<4, 0>(cyc, out, grid, reps, h2.data());
+        double c0 = run<0, 0>(cyc, out, grid, reps, h0.data());
+        const bool e3 = memcmp(h0.data(), h1.data(), 4 * 64 * grid) == 0, e4 = memcmp(h0.data(), h2.data(), 4 * 64 * grid) == 0;
+        printf("grid %4d pile-up chain: product %.1f, quads held %.1f (%s), + precomputed addresses %.1f (%s)\n", grid, c0,
+               c3, e3 ? "equal" : "DIFFER", c4, e4 ? "equal" : "DIFFER");
+      }
       double c0 = run<0, 0>(cyc, out, grid, reps, h0.data());
       double c1 = run<1, 0>(cyc, out, grid, reps, h1.data());
       double c2 = run<2, 0>(cyc, out, grid, reps, h2.data());
