@@ -15,6 +15,8 @@
 #   tools/gpu.sh stamps   <tag> [G=lanes] <envs...>  per-phase wave stamps (tools/stamps.py; stamps library prebuilt)
 #   tools/gpu.sh rehearse <tag>                 plain `bench.py --gpus 2` (it starts torchrun itself), both ranks on cuda:0 (gloo)
 #   tools/gpu.sh driver   <tag>                 the driver's own `bench.py --gpus 1 --steps 20 --warmup 5` line
+#   tools/gpu.sh ringpmc  <tag>                 FETCH/WRITE PMC + kernel trace of the frame-ring leg (lane-pair ring kernel)
+#   tools/gpu.sh groupprof <tag>                lane-group kernel at 4,096 / 8,192 envs: kernel trace + stamps (lib/exp/lib_stg.so)
 #   tools/gpu.sh policy   <tag>                 policy/rollout GPU tests + bench_policy + graph rollouts
 #
 # Several jobs in one call: tools/gpu.sh multi "suite r04a" "sq r04a_sq 65536" ...
@@ -214,6 +216,31 @@ tcc() {  # tag lib-name: HBM request-size split of the lane-pair step kernel (to
   done
   python tools/tcc_split.py $O ms_step_pair_kernel 65536 200 | tee $O/summary.json
   rm -rf $O/p1 $O/p2  # the raw per-dispatch CSVs exceed gpurun's 64-MiB copy-back
+}
+
+ringpmc() {  # tag: FETCH/WRITE passes and a kernel trace over a driver-window bench run WITH its frame-ring leg
+  local O=gpurun_out/$1; mkdir -p $O
+  local C
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/ring_$C -o run -- python bench.py --warmup 5 --steps 20 --no-cpu-baseline --fused 0 > $O/ring_$C.log 2>&1 \
+      || { echo "ring pmc $C failed"; tail -5 $O/ring_$C.log; return 1; }
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ring_trace -o run -- python bench.py --warmup 5 --steps 20 --no-cpu-baseline --fused 0 > $O/ring_trace.log 2>&1 \
+    || { echo "ring trace failed"; tail -5 $O/ring_trace.log; return 1; }
+  python tools/ring_pmc.py $O 65536 | tee $O/ring_summary.json
+}
+
+groupprof() {  # tag: the lane-group kernel at 4,096 and 8,192 envs: kernel trace (per-step and K-step), stamps (lib_stg)
+  local O=gpurun_out/$1; mkdir -p $O
+  local N
+  for N in 4096 8192; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/gtrace_$N -o run -- python bench.py --envs $N --no-cpu-baseline --no-ring-leg --fused 50 > $O/gtrace_$N.log 2>&1 \
+      || { echo "group trace $N failed"; tail -5 $O/gtrace_$N.log; return 1; }
+    grep -h "group" $O/gtrace_$N/run_kernel_stats.csv | cut -c1-60,160-260
+    timeout -k 10 240 python tools/stamps.py --lib marl-soccer_amd/lib/exp/lib_stg.so --envs $N --steps 300 --warmup 1000 --every 10 --out $O/gstamps_$N.json > $O/gstamps_$N.log 2>&1 \
+      || { echo "group stamps $N failed"; tail -5 $O/gstamps_$N.log; return 1; }
+    python -c "import json; d=json.load(open('$O/gstamps_$N.json')); print($N, d['launch'], 'mean', round(d['wave_cycles_mean']), 'worst', round(d.get('worst_wave_cycles_mean', 0)), {k: round(v['mean']) for k, v in d['phases'].items() if v['mean']}); t=d['timeline']; print({k: v for k, v in t.items() if k != 'waves_in_phase_per_us_bin'})"
+  done
 }
 
 driver() {  # the driver's own bench command, N = 1 (BENCH_rNN.json)

@@ -14,12 +14,15 @@ import sys
 
 def main(d, envs):
     out = {}
-    stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
-    for kernel in ("ms_step_kernel", "ms_step_ring_kernel"):
+    trace = "ring_trace" if os.path.isdir(os.path.join(d, "ring_trace")) else "trace"
+    fetch_dir = "ring_FETCH_SIZE" if trace == "ring_trace" else "pmc_fetch"
+    write_dir = "ring_WRITE_SIZE" if trace == "ring_trace" else "pmc_write"
+    stats = list(csv.DictReader(open(os.path.join(d, trace, "run_kernel_stats.csv"))))
+    for kernel in ("ms_step_kernel", "ms_step_ring_kernel", "ms_step_pair_kernel", "ms_step_pair_ring_kernel"):
         ks = [r for r in stats if kernel + "<" in r["Name"]]
-        fetch = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, "pmc_fetch", "run_counter_collection.csv")))
+        fetch = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, fetch_dir, "run_counter_collection.csv")))
                  if kernel + "<" in r["Kernel_Name"]]
-        write = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, "pmc_write", "run_counter_collection.csv")))
+        write = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, write_dir, "run_counter_collection.csv")))
                  if kernel + "<" in r["Kernel_Name"]]
         if not ks or not fetch or not write:
             continue
