@@ -646,6 +646,12 @@ __device__ __forceinline__ V2 div_nr2_pos(V2 n, float d, float r) {
   e = __builtin_elementwise_fma(nd, q, n);
   return __builtin_elementwise_fma(e, rv, q);
 }
+// div_k_nonneg of both components as packed fp32 (the magnitudes / 1000 of unit_mag2_pos); the same
+// operations per component, checked with the scalar forms by tools/div_check.hip
+__device__ __forceinline__ V2 div_k2_nonneg(V2 n, float d, float r) {
+  const V2 q = n * V2{r, r};
+  return __builtin_elementwise_fma(__builtin_elementwise_fma(V2{-d, -d}, q, n), V2{r, r}, q);
+}
 __device__ __forceinline__ void unit_mag_pos(float dx, float dy, float* o);
 __device__ __forceinline__ void unit_mag2_pos(float ax, float ay, float bx, float by, float* oa, float* ob) {
   const V2 X = v2(ax, bx), Y = v2(ay, by);
@@ -672,8 +678,7 @@ __device__ __forceinline__ void unit_mag2_pos(float ax, float ay, float bx, floa
   const float r1k = rcp_nr(1000.0f);
   V2 qm;
   if (MS_DIV_ONESTEP) {
-    const V2 q = N * V2{r1k, r1k};
-    qm = __builtin_elementwise_fma(__builtin_elementwise_fma(V2{-1000.0f, -1000.0f}, q, N), V2{r1k, r1k}, q);
+    qm = div_k2_nonneg(N, 1000.0f, r1k);
   } else {
     qm = div_nr2_pos(N, 1000.0f, r1k);
   }

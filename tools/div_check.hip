@@ -2,40 +2,48 @@
 //
 //   hipcc -O3 -ffp-contract=off --offload-arch=gfx950 -o div_check tools/div_check.hip && ./div_check
 //
-// For a divisor d and y = rcp_nr(d) (the kernels' refined reciprocal), q0 = n y, r = fma(-d, q0, n),
-// q1 = fma(r, y, q0) is compared bit for bit with the IEEE quotient n / d for EVERY fp32 numerator n
-// of a bit range (both signs), for the divisors the frame arithmetic divides by: 1000 (magnitudes),
-// 200 and 10 (the default obs_vmax, obs_wmax) and pi (angle_obs). Any mismatch is counted and the first
-// few are printed; a clean run over a domain proves the shorter sequence equal there.
+// For a divisor d and y = rcp_nr(d) (the kernels' refined reciprocal), the product's one-residual
+// quotient div_k(n, d, y) (q0 = n y, r = fma(-d, q0, n), q1 = fma(r, y, q0)) is compared bit for bit
+// with the IEEE quotient n / d for EVERY fp32 numerator n of a bit range (both signs), and for n >= +0
+// also div_k_nonneg and the packed div_k2_nonneg of unit_mag2_pos (both components), for the divisors
+// the frame arithmetic divides by: 1000 (magnitudes), 200 and 10 (the default obs_vmax, obs_wmax) and pi
+// (angle_obs). The functions are ms_device.h's own (included), so a change to them is what this checks.
+// Any mismatch is counted and the first few are printed; a clean run over a domain proves the shorter
+// sequence equal there.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
 #include <cstring>
 
-__device__ __forceinline__ float rcp_nr(float d) {
-  const float r = __builtin_amdgcn_rcpf(d);
-  const float e = __builtin_fmaf(-d, r, 1.0f);
-  return __builtin_fmaf(e, r, r);
-}
+// the product's own device functions (rcp_nr, div_k, div_k_nonneg, div_k2_nonneg), not copies
+#include "../marl-soccer_amd/csrc/ms_device.h"
 
 __global__ void check(float d, uint32_t lo, uint32_t hi, unsigned long long* bad, uint32_t* first) {
-  const float y = rcp_nr(d);
+  const float y = ms::rcp_nr(d);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= (uint64_t)(hi - lo); i += stride) {
     const uint32_t bits = lo + (uint32_t)i;
+    float qn[2];
 #pragma unroll
     for (int sg = 0; sg < 2; ++sg) {
       const float n = __uint_as_float(bits | (sg ? 0x80000000u : 0u));
       const float ref = n / d;
-      const float q0 = n * y;
-      const float r = __builtin_fmaf(-d, q0, n);
-      const float q1 = __builtin_fmaf(r, y, q0);
-      const bool same = __float_as_uint(q1) == __float_as_uint(ref) || (n == 0.0f && q1 == ref);
+      const float q1 = ms::div_k(n, d, y);
+      bool same = __float_as_uint(q1) == __float_as_uint(ref) || (n == 0.0f && q1 == ref);
+      if (sg == 0) {  // the non-negative forms (magnitudes): scalar and packed, this numerator paired with its neighbour
+        const float q2 = ms::div_k_nonneg(n, d, y);
+        const float nb = __uint_as_float(bits + 1u <= hi ? bits + 1u : bits);
+        const ms::V2 q3 = ms::div_k2_nonneg(ms::V2{n, nb}, d, y);
+        same = same && __float_as_uint(q2) == __float_as_uint(ref) && __float_as_uint(q3.x) == __float_as_uint(ref) &&
+               __float_as_uint(q3.y) == __float_as_uint(nb / d);
+      }
+      qn[sg] = q1;
       if (!same) {
         const unsigned long long k = atomicAdd(bad, 1ull);
         if (k < 4) first[k] = __float_as_uint(n);
       }
     }
+    (void)qn;
   }
 }
 
