@@ -1335,6 +1335,54 @@ __device__ __forceinline__ Params kernel_params(const Params& Pin) {
     return P;
   }
 }
+// The parameters a lane-pair or lane-group kernel steps with: PM 0 the kernel argument in the
+// kernel-argument segment itself (every such kernel takes (DevState, Params, ...), laid out as KArgHead; read
+// per phase: param_phase — a reference to the by-value parameter would be a copy in scratch), the
+// others kernel_params' folded constants
+struct KArgHead {
+  DevState S;
+  Params P;
+};
+template <int PM>
+__device__ __forceinline__ const Params& step_params(const Params& Pin, Params& tmp) {
+  if constexpr (PM == 0) {
+    const __attribute__((address_space(4))) char* ka =
+        (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+    return *(const Params*)(const __attribute__((address_space(4))) Params*)(ka + offsetof(KArgHead, P));
+  } else {
+    tmp = kernel_params<PM>(Pin);
+    return tmp;
+  }
+}
+
+// PM 0: the step's parameters are a phase-local copy (Pv), re-read from the kernel-argument
+// segment at every phase boundary through a pointer the compiler cannot see through: each phase
+// loads (s_load) only the fields it uses, at its start, instead of one load per field held in SGPRs
+// from its first to its last use across the step (the spills of the generic kernels). A copy, not
+// per-use loads: a per-lane select between two parameters loaded at the select would be folded into
+// one per-lane vector load from a selected address. (Pa must be the kernel argument in the argument
+// segment itself, pair_params; the default-physics kernels copy their folded constants.)
+__device__ __forceinline__ const Params* param_phase(const Params* p) {
+  auto q = (const __attribute__((address_space(4))) Params*)p;
+  asm volatile("" : "+s"(q));
+  return (const Params*)q;
+}
+
+// The K-step kernels' arguments as laid out in the kernel-argument segment (ms_step_pair_n_kernel;
+// ms_step_group_n_kernel adds `int solve` after them)
+struct KStepArgs {
+  DevState S;
+  Params P;
+  int K;
+  const float* actions;
+  float* obs;
+  float* rew;
+  uint8_t* term;
+  uint8_t* trunc;
+  int8_t* goal_out;
+  int32_t* score_out;
+  Counters* ctr;
+};
 // The first HBM batch of one state block (one wave's 64 envs): scalars, bodies, actions, the
 // previous step's arbiter-cache entries 0..KC-1 and PCG64. The scalars come first and alone
 // (fetch_scalars): the cache entries' addresses depend on them (parity bit, entry count).
