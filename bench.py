@@ -70,6 +70,9 @@ def parse():
                     help="ms_step kernel (SoccerBatch.set_lane_group): G = 2, 8 or 16 lanes per env, 0 one lane "
                          "per env, -1 automatic; default: the library's (8 lanes while envs x 8 fit the SIMDs, "
                          "else 2)")
+    ap.add_argument("--group-solve", type=int, default=0, metavar="M",
+                    help="diagnostic: the lane-group kernel's contact-solve schedule (SoccerBatch.set_group_solve): "
+                         "0 automatic (default), 1 serial halves, 2 dependency-level rounds")
     ap.add_argument("--generic", choices=("rewards", "physics"), default=None,
                     help="a non-default config: 'rewards' (ball_proximity_multiplier 0.003) runs the default-physics "
                          "kernels with runtime reward multipliers (ms_config_specialised 2), 'physics' "
@@ -269,6 +272,8 @@ def main():
              SoccerBatch(E, config=cfg, device=dev.index))
     if args.lane_group is not None and not ring:
         batch.set_lane_group(args.lane_group)
+    if args.group_solve and not ring:
+        batch.set_group_solve(args.group_solve)
     batch.reset(seed=19 + rank * E)  # env i of rank r seeded 19 + r*E + i (global index)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
@@ -429,6 +434,8 @@ def main():
         fb = SoccerBatch(E, config=cfg, device=dev.index)
         if args.lane_group is not None:
             fb.set_lane_group(args.lane_group)
+        if args.group_solve:
+            fb.set_group_solve(args.group_solve)
         fb.reset(seed=19)
         fsets = max(1, min(f_steps // K, int(args.action_gib * (1 << 30) // (E * 48 * K))))
         fpool = [torch.rand((K, E, 4, 3), device=dev, generator=gen) * 2 - 1 for _ in range(fsets)]
@@ -536,7 +543,10 @@ def main():
                                           "runtime reward multipliers", 0: "generic (every parameter from the kernel "
                                           "arguments)"}[batch.specialised],
                        **({"obs_layout": f"frame ring, R = {ring} (opt-in; obs is a strided (N, 4, 66) window)"}
-                          if ring else {})},
+                          if ring else {}),
+                       **({"group_solve": {1: "serial halves", 2: "dependency-level rounds"}.get(args.group_solve,
+                                                                                            args.group_solve)}
+                          if args.group_solve else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          # the HBM bytes rocprofv3 measured (traffic) over the same time: the
